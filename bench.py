@@ -1,0 +1,212 @@
+#!/usr/bin/env python
+"""Benchmark: signature-kernel Gram entries/s on MI355X (BASELINE.json metric).
+
+One step = one full normalised K(X) of SignatureRBF (reference gpsig/kernels.py:402-477) over the
+synthetic workload, inputs resident in HBM: lengthscale scaling, the per-level diagonal (for the
+normalisation), the Gram recursion kernel with the fused normalisation / sigma*variances / level-sum
+epilogue, and -- at N > 1 GPUs -- the RCCL all-gather of the row blocks plus the gfx950 mirror
+assembly, so every rank ends with the full N x N matrix ("scaling": "strong": the total Gram is fixed).
+
+    python bench.py                        # N=1, headline workload
+    torchrun --nproc-per-node 8 bench.py --gpus 8
+
+Prints ONE JSON line on rank 0 (contract in the task statement / DESIGN.md "Measurement").
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import multiprocessing as mp
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+WORKLOADS = {
+    # north_star target configuration (SURVEY.md 8 "H")
+    "H": dict(n=4096, l=128, d=5, m=5),
+    # BASELINE.json configs[1]
+    "C2": dict(n=1024, l=100, d=5, m=5),
+    # BASELINE.json configs[4] (8 GPUs)
+    "C5": dict(n=8192, l=128, d=8, m=6),
+}
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec (MI355X_MICROARCH.md chip table)
+
+
+def synthetic(n, l, d, seed=0):
+    """X = cumsum(N(0,1)) / sqrt(L*D), float32."""
+    rng = np.random.default_rng(seed)
+    return (np.cumsum(rng.standard_normal((n, l, d)), axis=1) / np.sqrt(l * d)).astype(np.float32)
+
+
+# ----------------------------------------------------------------------------- CPU baseline
+def _cpu_worker(args):
+    seconds, n_blk, l, d, m, seed = args
+    os.environ["OMP_NUM_THREADS"] = "1"
+    os.environ["OPENBLAS_NUM_THREADS"] = "1"
+    from oracle import kernels_ref as kr  # checker/baseline only (oracle is test infrastructure)
+    k = kr.SignatureKernelRef(l * d, d, m, normalization=False)
+    X = synthetic(2 * n_blk, l, d, seed).astype(np.float64)
+    t0 = time.perf_counter()
+    done = 0
+    while True:
+        k.K_seq(X[:n_blk], X[n_blk:])
+        done += n_blk * n_blk
+        if time.perf_counter() - t0 >= seconds:
+            break
+    return done, time.perf_counter() - t0
+
+
+def cpu_baseline(l, d, m, seconds=15.0, n_blk=8):
+    try:
+        cores = len(os.sched_getaffinity(0))
+    except AttributeError:  # pragma: no cover
+        cores = os.cpu_count() or 1
+    procs = max(1, min(16, cores))
+    with mp.get_context("spawn").Pool(procs) as pool:
+        res = pool.map(_cpu_worker, [(seconds, n_blk, l, d, m, 100 + i) for i in range(procs)])
+    entries = sum(r[0] for r in res)
+    wall = max(r[1] for r in res)
+    return dict(value=entries / wall, unit="entries/s", cores=procs, kind="port",
+                sample=(f"{procs} processes x {wall:.1f}s of {n_blk}x{n_blk}-pair raw per-level Gram blocks, "
+                        f"L={l}, D={d}, M={m}: oracle/kernels_ref.py float64 NumPy restatement of the "
+                        f"reference dataflow (materialised base-kernel tensor, exclusive cumsums)"))
+
+
+# ----------------------------------------------------------------------------- main
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--workload", default="H", choices=sorted(WORKLOADS))
+    ap.add_argument("--n", type=int)
+    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--traffic-json", default=None,
+                    help="per-launch HBM bytes of the Gram kernel from a PMC pass (profiles/*.json)")
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
+    dev = torch.device("cuda", local_rank)
+
+    import gpsig_amd
+    from gpsig_amd import _lib as L
+    from gpsig_amd import distributed as gdist
+    from gpsig_amd import ops
+
+    wl = dict(WORKLOADS[args.workload])
+    if args.n:
+        wl["n"] = args.n
+    n, l, d, m = wl["n"], wl["l"], wl["d"], wl["m"]
+    Xnp = synthetic(n, l, d)
+    X = torch.as_tensor(Xnp.reshape(n, l * d), device=dev)
+    kern = gpsig_amd.SignatureRBF(l * d, d, m)
+
+    # events around every launch of the dominant kernel (the Gram recursion), on its stream
+    ev = []
+    rows_done = [0]
+
+    def timed_compute(Xs, levels_out, rows, out, out_row0, **kw):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        r = ops.sig_gram(Xs, None, rows=rows, out=out, out_row0=out_row0, **kw)
+        e1.record()
+        ev.append((e0, e1))
+        rows_done[0] += rows[1] - rows[0]
+        return r
+
+    def step():
+        Xs = kern._prep(X)
+        rs = kern._rsqrt_diag(Xs)
+        return gdist.sharded_sym_gram(Xs, m, out_mode=L.OUT_NORM_SUM, compute=timed_compute, rs1=rs, rs2=rs,
+                                      scale=kern._scale_vec(dev), jitter=kern.jitter, order=kern.order,
+                                      base=kern.base, difference=kern.difference)
+
+    for _ in range(args.warmup):
+        K = step()
+    torch.cuda.synchronize()
+    ev.clear()
+    rows_done[0] = 0
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        K = step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([elapsed], device=dev, dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        elapsed = float(t.item())
+
+    # dominant-kernel roofline: algorithmic bytes per Gram entry
+    kern_ms = sum(a.elapsed_time(b) for a, b in ev)
+    launches = len(ev)
+    entries_per_launch = rows_done[0] * n / max(launches, 1)
+    b_entry = 4 * (l - 1) * (l - 1) + 4 * (m + 1)
+    avg_launch_s = kern_ms / 1e3 / max(launches, 1)
+    achieved = entries_per_launch * b_entry / avg_launch_s / 1e9
+    traffic = None
+    if args.traffic_json and os.path.exists(args.traffic_json):
+        with open(args.traffic_json) as f:
+            traffic = json.load(f).get("hbm_bytes_per_launch")
+
+    value = args.steps * n * n / elapsed
+    out = {
+        "metric": "sig-kernel Gram entries/sec (N, len L, dim D, level M); max-abs err vs ref",
+        "value": value,
+        "unit": "entries/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic random walks X = cumsum(N(0,1))/sqrt(L*D), seed 0 (SURVEY.md 8d)",
+        "config": {"workload": f"SignatureRBF K(X) normalised, N={n}, L={l}, D={d}, M={m}, order=1",
+                   "global_batch": n, "seq_len": l, "parallelism": f"row-shard{world}" if world > 1 else "single"},
+        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     "kernel": "sig_fo_kernel", "launch_ms": avg_launch_s * 1e3, "bytes_per_entry": b_entry,
+                     "entries_per_launch": entries_per_launch},
+    }
+    if rank == 0 and not args.no_check:
+        # parity on a bounded subsample: the normalised Gram restricted to a subset S of the sequences
+        # equals K(X[S]) (per-sequence diagonals), which the float64 oracle evaluates directly
+        from oracle import kernels_ref as kr
+        S = np.unique(np.linspace(0, n - 1, 40).astype(int))
+        Kref = kr.SignatureKernelRef(l * d, d, m).K(Xnp[S].astype(np.float64).reshape(len(S), -1))
+        got = K[torch.as_tensor(S, device=dev)][:, torch.as_tensor(S, device=dev)].double().cpu().numpy()
+        out["max_abs_err"] = float(np.abs(got - Kref).max())
+        out["max_abs_ref"] = float(np.abs(Kref).max())
+    if rank == 0 and world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(l, d, m, seconds=args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.barrier()
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,156 @@
+// gpsig_amd -- extern "C" entry points (include/gpsig_amd.h): argument checks, workspace carving,
+// tile counts, and dispatch to the templated kernels.  No allocation, no synchronisation.
+#include "sig_common.h"
+
+namespace gpsig {
+int features(const float *X, int n, int l, int d, int DP, float *F, hipStream_t s);
+int sig_fo_launch(const SigArgs &a, int DP, int seed, long long nblocks, hipStream_t s);
+int fo_lanes_per_pair(int l2);
+int sig_ho_launch(const SigArgs &a, int DP, int seed, long long nblocks, hipStream_t s);
+int ho_lanes_per_pair(int l2, int order, int M);
+int pde_launch(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int dyadic, int solver,
+               int pair_mode, int row_begin, int row_end, float *out, int out_row0, int out_rows,
+               long long out_ld, hipStream_t s);
+int sym_assemble_launch(const float *src, const long long *row_off, long long level_stride, int n, int levels,
+                        float *dst, hipStream_t s);
+}  // namespace gpsig
+
+using namespace gpsig;
+
+// Channel padding of the feature records: exact for the first-order kernels up to 6 channels,
+// multiples the instantiation tables cover otherwise (sig_fo_inst / sig_ho).
+static int pad_channels(int d, int order) {
+  if (order == 1 && d <= 6) return d;
+  if (order > 1 && d <= 4) return 4;
+  if (d <= 8) return 8;
+  if (d <= 16) return 16;
+  if (d <= 32) return 32;
+  return 0;
+}
+
+static size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
+
+static size_t feat_bytes(int n, int l, int d) {
+  const int DP = pad_channels(d, 2);  // the wider of the two paddings
+  if (DP == 0) return 0;
+  return align256((size_t)n * l * feat_stride(DP) * sizeof(float));
+}
+
+static int seed_of(int base_kind, int difference) {
+  if (base_kind == GPSIG_BASE_RBF) return difference ? SEED_RBF_DIFF : SEED_RBF_POINT;
+  if (base_kind == GPSIG_BASE_LINEAR) return difference ? SEED_LIN_DIFF : SEED_LIN_POINT;
+  return -1;
+}
+
+extern "C" size_t gpsig_sig_workspace_bytes(int n1, int l1, int n2, int l2, int d) {
+  return feat_bytes(n1, l1, d) + feat_bytes(n2, l2, d);
+}
+
+static inline long long upper_prefix(long long r, long long ntb, long long k) { return r * ntb - k * r * (r - 1) / 2; }
+
+extern "C" int gpsig_sig_gram(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int num_levels,
+                              int order, int base_kind, int difference, int pair_mode, int row_begin, int row_end,
+                              const float *rs1, const float *rs2, const float *scale, float jitter, int out_mode,
+                              float *out, int out_row0, int out_rows, void *workspace, size_t workspace_bytes,
+                              gpsig_stream_t stream) {
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (!X || !Y || !out || n1 <= 0 || n2 <= 0 || d <= 0 || num_levels < 1) return GPSIG_EINVAL;
+  if (l1 < 1 || l2 < 1 || (difference && (l1 < 2 || l2 < 2))) return GPSIG_EINVAL;
+  if (pair_mode < GPSIG_PAIRS_RECT || pair_mode > GPSIG_PAIRS_DIAG) return GPSIG_EINVAL;
+  if (row_begin < 0 || row_end > n1 || row_begin > row_end) return GPSIG_EINVAL;
+  if (pair_mode != GPSIG_PAIRS_RECT && (n1 != n2 || l1 != l2)) return GPSIG_EINVAL;
+  if (out_mode < GPSIG_OUT_LEVELS || out_mode > GPSIG_OUT_RSQRT) return GPSIG_EINVAL;
+  if (out_mode == GPSIG_OUT_RSQRT && pair_mode != GPSIG_PAIRS_DIAG) return GPSIG_EINVAL;
+  if ((rs1 == nullptr) != (rs2 == nullptr)) return GPSIG_EINVAL;
+  if (order < 1) return GPSIG_EINVAL;
+  const int seed = seed_of(base_kind, difference);
+  const int DP = pad_channels(d, order);
+  if (seed < 0 || DP == 0) return GPSIG_EUNSUPPORTED;
+  if (row_end == row_begin) return GPSIG_OK;
+
+  const bool same = (X == Y && n1 == n2 && l1 == l2);
+  const size_t fx_b = align256((size_t)n1 * l1 * feat_stride(DP) * sizeof(float));
+  const size_t fy_b = same ? 0 : align256((size_t)n2 * l2 * feat_stride(DP) * sizeof(float));
+  if (!workspace || workspace_bytes < fx_b + fy_b) return GPSIG_EWORKSPACE;
+  float *FX = static_cast<float *>(workspace);
+  float *FY = same ? FX : reinterpret_cast<float *>(static_cast<char *>(workspace) + fx_b);
+  int rc = features(X, n1, l1, d, DP, FX, s);
+  if (rc) return rc;
+  if (!same && (rc = features(Y, n2, l2, d, DP, FY, s))) return rc;
+
+  SigArgs a{};
+  a.FX = FX;
+  a.FY = FY;
+  a.n1 = n1; a.l1 = l1; a.n2 = n2; a.l2 = l2;
+  a.fs = feat_stride(DP);
+  a.M = num_levels;
+  a.order = order;
+  a.pair_mode = pair_mode;
+  a.row_begin = row_begin;
+  a.row_end = row_end;
+  a.rs1 = rs1; a.rs2 = rs2; a.scale = scale;
+  a.jitter = jitter;
+  a.out_mode = out_mode;
+  a.out = out;
+  a.out_row0 = out_row0;
+  a.out_rows = out_rows;
+  a.out_ld = n2;
+  a.out_lvl = (long long)out_rows * n2;
+
+  const int LP = (order == 1) ? fo_lanes_per_pair(l2) : ho_lanes_per_pair(l2, order, num_levels);
+  if (LP == 0) return GPSIG_EUNSUPPORTED;
+  const int G = 64 / LP;
+  long long nblocks = 0;
+  if (pair_mode == GPSIG_PAIRS_DIAG) {
+    a.out_lvl = n1;
+    nblocks = (row_end - row_begin + 3) / 4;
+  } else {
+    const int ta0 = row_begin / 4, ta1 = (row_end + 3) / 4;
+    const int ntb = (n2 + G - 1) / G;
+    a.tiles_a0 = ta0;
+    a.ntb = ntb;
+    if (pair_mode == GPSIG_PAIRS_RECT) {
+      nblocks = (long long)(ta1 - ta0) * ntb;
+    } else {
+      const int k = 4 / G;
+      a.tile_base = upper_prefix(ta0, ntb, k);
+      nblocks = upper_prefix(ta1, ntb, k) - a.tile_base;
+    }
+  }
+  if (nblocks > 0x7fffffffLL) return GPSIG_EUNSUPPORTED;
+  return (order == 1) ? sig_fo_launch(a, DP, seed, nblocks, s) : sig_ho_launch(a, DP, seed, nblocks, s);
+}
+
+extern "C" int gpsig_sig_diag(const float *X, int n, int l, int d, int num_levels, int order, int base_kind,
+                              int difference, float jitter, int out_mode, float *out, void *workspace,
+                              size_t workspace_bytes, gpsig_stream_t stream) {
+  if (out_mode != GPSIG_OUT_LEVELS && out_mode != GPSIG_OUT_RSQRT) return GPSIG_EINVAL;
+  return gpsig_sig_gram(X, n, l, X, n, l, d, num_levels, order, base_kind, difference, GPSIG_PAIRS_DIAG, 0, n,
+                        nullptr, nullptr, nullptr, jitter, out_mode, out, 0, n, workspace, workspace_bytes, stream);
+}
+
+extern "C" int gpsig_pde_gram(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int dyadic,
+                              int solver, int pair_mode, int row_begin, int row_end, float *out, int out_row0,
+                              int out_rows, gpsig_stream_t stream) {
+  if (!X || !Y || !out || n1 <= 0 || n2 <= 0 || d <= 0 || l1 < 2 || l2 < 2) return GPSIG_EINVAL;
+  if (dyadic < 0 || dyadic > 6 || (solver != 0 && solver != 1)) return GPSIG_EINVAL;
+  if (pair_mode < GPSIG_PAIRS_RECT || pair_mode > GPSIG_PAIRS_DIAG) return GPSIG_EINVAL;
+  if (row_begin < 0 || row_end > n1 || row_begin > row_end) return GPSIG_EINVAL;
+  if (pair_mode != GPSIG_PAIRS_RECT && (n1 != n2 || l1 != l2)) return GPSIG_EINVAL;
+  if (row_end == row_begin) return GPSIG_OK;
+  return pde_launch(X, n1, l1, Y, n2, l2, d, dyadic, solver, pair_mode, row_begin, row_end, out, out_row0,
+                    out_rows, n2, reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" int gpsig_pde_diag(const float *X, int n, int l, int d, int dyadic, int solver, float *out,
+                              gpsig_stream_t stream) {
+  return gpsig_pde_gram(X, n, l, X, n, l, d, dyadic, solver, GPSIG_PAIRS_DIAG, 0, n, out, 0, n, stream);
+}
+
+extern "C" int gpsig_sym_assemble(const float *src, const long long *row_off, long long level_stride, int n,
+                                  int levels, float *dst, gpsig_stream_t stream) {
+  if (!src || !dst || !row_off || n <= 0 || levels <= 0 || level_stride < 0) return GPSIG_EINVAL;
+  return sym_assemble_launch(src, row_off, level_stride, n, levels, dst, reinterpret_cast<hipStream_t>(stream));
+}
+
+extern "C" const char *gpsig_version(void) { return "gpsig_amd 0.1 (gfx950)"; }

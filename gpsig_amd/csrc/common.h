@@ -1,0 +1,78 @@
+// gpsig_amd -- shared device helpers for the gfx950 (CDNA4) signature-kernel kernels.
+//
+// Wave64 everywhere: cross-lane steps use DPP (row_shr / row_bcast / wave_shl), which on
+// gfx950 are single VALU-issue operations, instead of LDS round trips.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/gpsig_amd.h"
+
+#define GPSIG_DEV __device__ __forceinline__
+
+namespace gpsig {
+
+// ---------------------------------------------------------------------------------------------
+// DPP cross-lane helpers (gfx9 encodings: row_shr:n = 0x110|n, row_bcast:15 = 0x142,
+// row_bcast:31 = 0x143, wave_shl:1 = 0x130, wave_shr:1 = 0x138).
+template <int CTRL, int ROW_MASK = 0xF, int BANK_MASK = 0xF, bool BOUND_ZERO = true>
+GPSIG_DEV float dpp_f(float v) {
+  return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROW_MASK,
+                                                               BANK_MASK, BOUND_ZERO));
+}
+template <int CTRL, int ROW_MASK = 0xF, int BANK_MASK = 0xF, bool BOUND_ZERO = true>
+GPSIG_DEV double dpp_d(double v) {
+  const uint64_t u = __builtin_bit_cast(uint64_t, v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)u, CTRL, ROW_MASK, BANK_MASK, BOUND_ZERO);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(uint32_t)(u >> 32), CTRL, ROW_MASK, BANK_MASK, BOUND_ZERO);
+  return __builtin_bit_cast(double, ((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
+}
+
+// Inclusive prefix sum over aligned groups of LP lanes (LP = 16, 32 or 64).
+template <int LP>
+GPSIG_DEV float group_incl_scan(float v) {
+  static_assert(LP == 16 || LP == 32 || LP == 64, "LP");
+  v += dpp_f<0x111>(v);
+  v += dpp_f<0x112>(v);
+  v += dpp_f<0x114>(v);
+  v += dpp_f<0x118>(v);
+  if constexpr (LP >= 32) v += dpp_f<0x142, 0xA>(v);
+  if constexpr (LP >= 64) v += dpp_f<0x143, 0xC>(v);
+  return v;
+}
+
+// Value of lane (lane+1) of the wave (0 for lane 63).
+GPSIG_DEV float lane_next(float v) { return dpp_f<0x130>(v); }
+// Value of lane (lane-1) of the wave (`edge` for lane 0 is handled by the caller).
+GPSIG_DEV float lane_prev(float v) { return dpp_f<0x138>(v); }
+GPSIG_DEV double lane_prev(double v) { return dpp_d<0x138>(v); }
+
+// Sum over an aligned group of LP lanes, result in every lane of the group.
+template <int LP>
+GPSIG_DEV float group_sum(float v) {
+#pragma unroll
+  for (int o = LP / 2; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+GPSIG_DEV int wave_uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
+
+// ---------------------------------------------------------------------------------------------
+// expm1 on |x| <= 0.5 as x * P5(x): minimax (Lawson) fit of expm1(x)/x on [-0.5, 0.5], max
+// relative error 2.2e-7 in fp32 with FMA Horner (tests/test_numerics.py pins it).  Only used where
+// the caller has already checked |x| < EM1_TAU; outside that range the value is discarded.
+constexpr float EM1_TAU = 0.5f;
+GPSIG_DEV float em1_small(float x) {
+  float p = 1.388882549e-03f;
+  p = __builtin_fmaf(p, x, 8.407682727e-03f);
+  p = __builtin_fmaf(p, x, 4.166870013e-02f);
+  p = __builtin_fmaf(p, x, 1.666597426e-01f);
+  p = __builtin_fmaf(p, x, 4.999998314e-01f);
+  p = __builtin_fmaf(p, x, 1.000000095e+00f);
+  return p * x;
+}
+
+// exp(x) = 2^(x log2 e) on the hardware transcendental unit (v_exp_f32, ~1 ulp).
+GPSIG_DEV float fast_exp(float x) { return __builtin_amdgcn_exp2f(x * 1.4426950408889634f); }
+
+}  // namespace gpsig

@@ -1,0 +1,247 @@
+// gpsig_amd -- Goursat-PDE (untruncated) signature kernel on gfx950.
+//
+// Replaces gpsig/sigKer_fast.pyx:15-62 (CPU, k(x,x) only) and the CUDA op
+// gpsig/covariance_op/untrunc_cov_op_gpu.cu:5-94 (one 1024-thread block per pair, one thread per
+// grid row, a __syncthreads per anti-diagonal, every cell through global memory).
+//
+// Here one wave64 solves one pair entirely in registers.  Lane l owns W consecutive fine columns and
+// sweeps the rows with a one-step skew: at step s it updates row i = s - l, taking the left boundary
+// K[i+1][lW] from lane l-1 (computed one step earlier) through a single DPP wave_shr:1, and the
+// corner K[i][lW] from the previous step's left boundary.  No LDS traffic for the solution, no
+// barriers, no 1024-row cap (kernels_pde.py:53); the coarse increments of x (the only lane-varying
+// input) sit in LDS, y's increments for the lane's columns in registers.
+//   inc(i, j) = <dx_{i>>n}, dy_{j>>n}> / 4^n                         (sigKer_fast.pyx:35-43)
+//   solver 1: K[i+1][j+1] = (K[i][j+1] + K[i+1][j]) (1 + inc/2 + inc^2/12) - K[i][j] (1 - inc^2/12)
+//   solver 0: K[i+1][j+1] = K[i][j+1] + K[i+1][j] + K[i][j] (inc - 1)
+// In DIAG mode with solver 0 the diagonal cells take the solver-1 update, as sigKer_fast.pyx:59 does.
+#include "sig_common.h"
+
+namespace gpsig {
+
+struct PdeArgs {
+  const float *X, *Y;
+  int n1, l1, n2, l2, d;
+  int dyadic, solver;
+  int pair_mode, row_begin, row_end;
+  int ntb, tiles_a0;
+  long long tile_base;
+  float *out;
+  int out_row0, out_rows;
+  long long out_ld;
+};
+
+template <typename T, int DP, int W>
+__global__ __launch_bounds__(256) void pde_kernel(PdeArgs p) {
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int lane = threadIdx.x & 63;
+  const int wave = wave_uniform(threadIdx.x >> 6);
+
+  int a, b;
+  if (p.pair_mode == GPSIG_PAIRS_DIAG) {
+    a = p.row_begin + (int)blockIdx.x * 4 + wave;
+    b = a;
+  } else {
+    int ta, tb;
+    if (p.pair_mode == GPSIG_PAIRS_UPPER) {
+      const Tile t = upper_tile(p.tile_base + (long long)blockIdx.x, p.ntb, 4);
+      ta = t.ta;
+      tb = t.tb;
+    } else {
+      ta = p.tiles_a0 + (int)blockIdx.x / p.ntb;
+      tb = (int)blockIdx.x % p.ntb;
+    }
+    a = ta * 4 + wave;
+    b = tb;
+  }
+  // wave-uniform validity; every wave still reaches the LDS barrier below
+  bool ok = a >= p.row_begin && a < p.row_end && b < p.n2;
+  if (p.pair_mode == GPSIG_PAIRS_UPPER && b < a) ok = false;
+  if (!ok) { a = p.row_begin; b = p.pair_mode == GPSIG_PAIRS_RECT ? 0 : a; }
+
+  const int n = p.dyadic;
+  const int rep = 1 << n;
+  const T inv_factor = (T)1.0 / (T)(1 << (2 * n));
+  const int I = rep * (p.l1 - 1), J = rep * (p.l2 - 1);
+  const int d = p.d;
+  const float *x = p.X + (long long)a * p.l1 * d;
+  const float *y = p.Y + (long long)b * p.l2 * d;
+
+  // coarse increments of x in this wave's LDS slice: (l1-1) x DP
+  float *dxs = lds + (size_t)wave * (p.l1 - 1) * DP;
+  for (int r = lane; r < p.l1 - 1; r += 64)
+#pragma unroll
+    for (int k = 0; k < DP; ++k) dxs[r * DP + k] = k < d ? x[(r + 1) * d + k] - x[r * d + k] : 0.0f;
+
+  // y increments for this lane's fine columns c = lane*W + w (coarse column c >> n)
+  float dy[W][DP];
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    int cj = (lane * W + w) >> n;
+    cj = cj < p.l2 - 2 ? cj : p.l2 - 2;
+#pragma unroll
+    for (int k = 0; k < DP; ++k) dy[w][k] = k < d ? y[(cj + 1) * d + k] - y[cj * d + k] : 0.0f;
+  }
+  __syncthreads();
+  if (!ok) return;
+
+  const bool hybrid = (p.pair_mode == GPSIG_PAIRS_DIAG) && p.solver == 0;
+  T up[W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) up[w] = (T)1;
+  T last = (T)1;   // K[i+1][lW+W] of this lane's most recent row (boundary 1 before it starts)
+  T left_prev = (T)1;
+  const int lanes_used = (J + W - 1) / W;
+  const int nsteps = I + lanes_used - 1;
+  for (int s = 0; s < nsteps; ++s) {
+    T left = lane_prev(last);
+    if (lane == 0) left = (T)1;
+    const T corner0 = left_prev;
+    left_prev = left;
+    const int i = s - lane;
+    if (i >= 0 && i < I && lane < lanes_used) {
+      const float *dxr = dxs + (i >> n) * DP;
+      float dxv[DP];
+#pragma unroll
+      for (int k = 0; k < DP; ++k) dxv[k] = dxr[k];
+      T lft = left, cor = corner0;
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        const int c = lane * W + w;
+        float incf = 0.0f;
+#pragma unroll
+        for (int k = 0; k < DP; ++k) incf = __builtin_fmaf(dxv[k], dy[w][k], incf);
+        const T inc = (T)incf * inv_factor;
+        const T upw = up[w];
+        T kn;
+        if (p.solver == 1 || (hybrid && c == i)) {
+          const T inc2 = inc * inc;
+          const T A = (T)1 + (T)0.5 * inc + (T)(1.0 / 12) * inc2;
+          const T B = (T)1 - (T)(1.0 / 12) * inc2;
+          kn = (upw + lft) * A - cor * B;
+        } else {
+          kn = (upw + lft) + cor * (inc - (T)1);
+        }
+        if (c < J) {
+          cor = upw;
+          lft = kn;
+          up[w] = kn;
+        }
+      }
+      last = lft;
+    }
+  }
+  // final corner K[I][J]: fine column J-1 -> lane (J-1)/W, slot (J-1)%W
+  const int owner = (J - 1) / W, slot = (J - 1) % W;
+  T res = (T)0;
+#pragma unroll
+  for (int w = 0; w < W; ++w)
+    if (w == slot) res = up[w];
+  if (lane == owner) {
+    const float v = (float)res;
+    if (p.pair_mode == GPSIG_PAIRS_DIAG) {
+      p.out[a] = v;
+    } else {
+      if (a >= p.out_row0 && a < p.out_row0 + p.out_rows) p.out[(long long)(a - p.out_row0) * p.out_ld + b] = v;
+      if (p.pair_mode == GPSIG_PAIRS_UPPER && a != b && b >= p.out_row0 && b < p.out_row0 + p.out_rows)
+        p.out[(long long)(b - p.out_row0) * p.out_ld + a] = v;
+    }
+  }
+}
+
+template <typename T, int DP, int W>
+static int launch_pde(const PdeArgs &a, long long nblocks, hipStream_t s) {
+  if constexpr (W * DP > 128) {
+    return GPSIG_EUNSUPPORTED;
+  } else {
+    const size_t lds = (size_t)4 * (a.l1 - 1) * DP * sizeof(float);
+    if (lds > 64 * 1024) return GPSIG_EUNSUPPORTED;
+    hipLaunchKernelGGL((pde_kernel<T, DP, W>), dim3((unsigned)nblocks), dim3(256), lds, s, a);
+    return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
+  }
+}
+
+template <typename T, int DP>
+static int pde_w(const PdeArgs &a, long long nblocks, int J, hipStream_t s) {
+  if (J <= 64) return launch_pde<T, DP, 1>(a, nblocks, s);
+  if (J <= 128) return launch_pde<T, DP, 2>(a, nblocks, s);
+  if (J <= 256) return launch_pde<T, DP, 4>(a, nblocks, s);
+  if (J <= 512) return launch_pde<T, DP, 8>(a, nblocks, s);
+  if (J <= 1024) return launch_pde<T, DP, 16>(a, nblocks, s);
+  return GPSIG_EUNSUPPORTED;
+}
+
+int pde_launch(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int dyadic, int solver,
+               int pair_mode, int row_begin, int row_end, float *out, int out_row0, int out_rows,
+               long long out_ld, hipStream_t s) {
+  PdeArgs a{};
+  a.X = X; a.Y = Y;
+  a.n1 = n1; a.l1 = l1; a.n2 = n2; a.l2 = l2; a.d = d;
+  a.dyadic = dyadic; a.solver = solver;
+  a.pair_mode = pair_mode; a.row_begin = row_begin; a.row_end = row_end;
+  a.out = out; a.out_row0 = out_row0; a.out_rows = out_rows; a.out_ld = out_ld;
+  long long nblocks;
+  if (pair_mode == GPSIG_PAIRS_DIAG) {
+    nblocks = (row_end - row_begin + 3) / 4;
+  } else {
+    const int ta0 = row_begin / 4, ta1 = (row_end + 3) / 4;
+    a.ntb = n2;
+    a.tiles_a0 = ta0;
+    if (pair_mode == GPSIG_PAIRS_RECT) {
+      nblocks = (long long)(ta1 - ta0) * n2;
+    } else {
+      auto P = [&](long long r) { return r * (long long)n2 - 4LL * r * (r - 1) / 2; };
+      a.tile_base = P(ta0);
+      nblocks = P(ta1) - a.tile_base;
+    }
+  }
+  if (nblocks <= 0) return GPSIG_OK;
+  const int J = (1 << dyadic) * (l2 - 1);
+  using T = double;  // fp64 solution grid (the reference's float64), fp32 increments (as the CUDA op, .cu:27)
+  switch (d <= 8 ? d : (d <= 16 ? 16 : 0)) {
+#define CASE(v) \
+  case v: return pde_w<T, v>(a, nblocks, J, s);
+    CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) CASE(16)
+#undef CASE
+    default: return GPSIG_EUNSUPPORTED;
+  }
+}
+
+// ------------------------------------------------------------------------------------ assembly
+// dst[l][a][b] = row a's value at column b for b >= a, else row b's value at column a (the mirror).
+// 32x32 tiles; the mirrored (lower) tiles go through LDS so both the read and the write are coalesced.
+__global__ __launch_bounds__(256) void sym_assemble_kernel(const float *__restrict__ src,
+                                                           const long long *__restrict__ row_off,
+                                                           long long level_stride, int n, float *__restrict__ dst) {
+  __shared__ float tile[32][33];
+  const int lvl = blockIdx.z;
+  const int bi = blockIdx.y, bj = blockIdx.x;  // dst tile rows bi*32.., cols bj*32..
+  const float *S = src + (long long)lvl * level_stride;
+  float *Dd = dst + (long long)lvl * n * n;
+  const int tx = threadIdx.x & 31, ty = threadIdx.x >> 5;  // 32 x 8
+  if (bj >= bi) {
+    for (int r = ty; r < 32; r += 8) {
+      const int a = bi * 32 + r, b = bj * 32 + tx;
+      if (a < n && b < n) Dd[(long long)a * n + b] = (b >= a) ? S[row_off[a] + b] : S[row_off[b] + a];
+    }
+  } else {
+    // lower tile: dst[a][b] = row b's column a; read rows b (tile columns) coalesced along a
+    for (int r = ty; r < 32; r += 8) {
+      const int brow = bj * 32 + r, acol = bi * 32 + tx;
+      tile[r][tx] = (brow < n && acol < n) ? S[row_off[brow] + acol] : 0.0f;
+    }
+    __syncthreads();
+    for (int r = ty; r < 32; r += 8) {
+      const int a = bi * 32 + r, b = bj * 32 + tx;
+      if (a < n && b < n) Dd[(long long)a * n + b] = tile[tx][r];
+    }
+  }
+}
+
+int sym_assemble_launch(const float *src, const long long *row_off, long long level_stride, int n, int levels,
+                        float *dst, hipStream_t s) {
+  const int nt = (n + 31) / 32;
+  hipLaunchKernelGGL(sym_assemble_kernel, dim3(nt, nt, levels), dim3(256), 0, s, src, row_off, level_stride, n, dst);
+  return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
+}
+
+}  // namespace gpsig

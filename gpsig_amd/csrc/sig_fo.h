@@ -1,0 +1,170 @@
+// gpsig_amd -- first-order truncated signature kernel Gram on gfx950 (kernel template).
+//
+// Replaces, for order == 1, the dataflow of gpsig/kernels.py:209-238 (_K_seq) +
+// gpsig/signature_algs.py:8-35 (signature_kern_first_order):
+//     dM = second difference of the base-kernel grid M(x_i, y_j)        (signature_algs.py:26)
+//     K_1 = sum dM,  R_m = dM * cumsum_x(cumsum_x(R_{m-1})), K_m = sum R_m   (:28-33)
+// without materialising M or R: a group of LP lanes owns one pair (a, b) and streams the rows i of
+// the dM grid; each lane keeps W columns j.  Per row and level, the exclusive 2-D prefix
+// S_m(i, j) = sum_{i'<i, j'<j} R_m(i', j') is the exclusive scan over j of the running column sums
+// C_m(j) = sum_{i'<i} R_m(i', j): per pair the state is M x W registers per lane and the only
+// cross-lane traffic is one DPP scan per level per row (the M-1 scans of a row are independent, so
+// they interleave).  K_m = sum_j C_m(j) at the end.  The seed (base-kernel second difference,
+// including the fp32-stable RBF form) is RowSeed in sig_common.h.
+#pragma once
+#include "sig_common.h"
+
+namespace gpsig {
+
+template <int DP, int W, int LP, int M, int SEED>
+__global__ __launch_bounds__(256) void sig_fo_kernel(SigArgs p) {
+  using Seed = RowSeed<DP, W, SEED>;
+  constexpr int FS = feat_stride(DP);
+  constexpr int G = 64 / LP;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = wave_uniform(threadIdx.x >> 6);
+  const int g = lane / LP;
+  const int gl = lane % LP;
+
+  // ---- which pair
+  int a, b;
+  if (p.pair_mode == GPSIG_PAIRS_DIAG) {
+    a = p.row_begin + (int)blockIdx.x * 4 + wave;
+    b = a;
+    if (a >= p.row_end) return;
+  } else {
+    int ta, tb;
+    if (p.pair_mode == GPSIG_PAIRS_UPPER) {
+      const Tile t = upper_tile(p.tile_base + (long long)blockIdx.x, p.ntb, 4 / G);
+      ta = t.ta;
+      tb = t.tb;
+    } else {
+      ta = p.tiles_a0 + (int)blockIdx.x / p.ntb;
+      tb = (int)blockIdx.x % p.ntb;
+    }
+    a = ta * 4 + wave;
+    b = tb * G + g;
+    if (a < p.row_begin || a >= p.row_end) return;  // wave-uniform
+  }
+  bool pair_ok = b < p.n2;
+  if (p.pair_mode == GPSIG_PAIRS_UPPER) pair_ok = pair_ok && b >= a;
+  if (p.pair_mode == GPSIG_PAIRS_DIAG) pair_ok = (g == 0);
+  const int bl = b < p.n2 ? b : p.n2 - 1;
+
+  const float *__restrict__ fx = p.FX + (long long)a * p.l1 * FS;
+  const float *__restrict__ fy = p.FY + (long long)bl * p.l2 * FS;
+
+  Seed seed;
+  seed.init(fx, fy, gl, p.l2);
+
+  float C[M][W];
+#pragma unroll
+  for (int m = 0; m < M; ++m)
+#pragma unroll
+    for (int w = 0; w < W; ++w) C[m][w] = 0.0f;
+
+  const int nrows = Seed::DIFF ? p.l1 - 1 : p.l1;
+  RowData<DP> rd;
+  rd.load(fx, 0, SEED);
+  for (int i = 0; i < nrows; ++i) {
+    // prefetch the next row's wave-uniform record (scalar loads) so their latency hides here
+    RowData<DP> rn;
+    rn.load(fx, i + 1 < nrows ? i + 1 : i, SEED);
+
+    float dM[W];
+    seed.row(rd, dM);
+
+    // ---- level recursion: S_m = exclusive prefix over (rows < i, cols < j) of R_m
+    float S[M > 1 ? M - 1 : 1][W];
+#pragma unroll
+    for (int m = 0; m + 1 < M; ++m) {
+      float t[W];
+      t[0] = C[m][0];
+#pragma unroll
+      for (int w = 1; w < W; ++w) t[w] = t[w - 1] + C[m][w];
+      const float incl = group_incl_scan<LP>(t[W - 1]);
+      const float base = incl - t[W - 1];
+      S[m][0] = base;
+#pragma unroll
+      for (int w = 1; w < W; ++w) S[m][w] = base + t[w - 1];
+    }
+#pragma unroll
+    for (int w = 0; w < W; ++w) C[0][w] += dM[w];
+#pragma unroll
+    for (int m = 0; m + 1 < M; ++m)
+#pragma unroll
+      for (int w = 0; w < W; ++w) C[m + 1][w] = __builtin_fmaf(dM[w], S[m][w], C[m + 1][w]);
+    rd = rn;
+  }
+
+  // ---- epilogue: K_m = sum_j C_m(j)
+  float K[M + 1];
+  K[0] = 1.0f;
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    float s = 0.0f;
+#pragma unroll
+    for (int w = 0; w < W; ++w) s += C[m][w];
+    K[m + 1] = group_sum<LP>(s);
+  }
+  if (gl == 0 && pair_ok) store_pair<M>(p, a, b, K);
+}
+
+// Column geometry: W columns per lane, LP lanes per pair; capacity LP*W >= points per sequence.
+struct Geo { int W, LP; };
+inline Geo fo_geometry(int l2) {
+  if (l2 <= 64) return {4, 16};
+  if (l2 <= 128) return {4, 32};
+  if (l2 <= 256) return {4, 64};
+  if (l2 <= 512) return {8, 64};
+  return {0, 0};
+}
+constexpr int FO_MAX_LEVELS = 8;
+
+template <int DP, int W, int LP, int M, int SEED>
+int launch_fo(const SigArgs &a, long long nblocks, hipStream_t s) {
+  if (nblocks <= 0) return GPSIG_OK;
+  hipLaunchKernelGGL((sig_fo_kernel<DP, W, LP, M, SEED>), dim3((unsigned)nblocks), dim3(256), 0, s, a);
+  return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
+}
+
+template <int DP, int M, int SEED>
+int fo_geo(const SigArgs &a, long long nblocks, hipStream_t s) {
+  const Geo geo = fo_geometry(a.l2);
+  if (geo.W == 4 && geo.LP == 16) return launch_fo<DP, 4, 16, M, SEED>(a, nblocks, s);
+  if (geo.W == 4 && geo.LP == 32) return launch_fo<DP, 4, 32, M, SEED>(a, nblocks, s);
+  if (geo.W == 4 && geo.LP == 64) return launch_fo<DP, 4, 64, M, SEED>(a, nblocks, s);
+  if (geo.W == 8 && geo.LP == 64) return launch_fo<DP, 8, 64, M, SEED>(a, nblocks, s);
+  return GPSIG_EUNSUPPORTED;
+}
+
+template <int DP, int SEED>
+int fo_levels(const SigArgs &a, long long nblocks, hipStream_t s) {
+  switch (a.M) {
+    case 1: return fo_geo<DP, 1, SEED>(a, nblocks, s);
+    case 2: return fo_geo<DP, 2, SEED>(a, nblocks, s);
+    case 3: return fo_geo<DP, 3, SEED>(a, nblocks, s);
+    case 4: return fo_geo<DP, 4, SEED>(a, nblocks, s);
+    case 5: return fo_geo<DP, 5, SEED>(a, nblocks, s);
+    case 6: return fo_geo<DP, 6, SEED>(a, nblocks, s);
+    case 7: return fo_geo<DP, 7, SEED>(a, nblocks, s);
+    case 8: return fo_geo<DP, 8, SEED>(a, nblocks, s);
+    default: return GPSIG_EUNSUPPORTED;
+  }
+}
+
+// One explicit instantiation per channel count lives in its own translation unit
+// (sig_fo_inst.hip compiled with -DGPSIG_DP=...), so the instantiations build in parallel.
+template <int DP>
+int sig_fo_launch_dp(const SigArgs &a, int seed, long long nblocks, hipStream_t s) {
+  switch (seed) {
+    case SEED_RBF_DIFF: return fo_levels<DP, SEED_RBF_DIFF>(a, nblocks, s);
+    case SEED_LIN_DIFF: return fo_levels<DP, SEED_LIN_DIFF>(a, nblocks, s);
+    case SEED_RBF_POINT: return fo_levels<DP, SEED_RBF_POINT>(a, nblocks, s);
+    case SEED_LIN_POINT: return fo_levels<DP, SEED_LIN_POINT>(a, nblocks, s);
+    default: return GPSIG_EUNSUPPORTED;
+  }
+}
+
+}  // namespace gpsig

@@ -1,0 +1,76 @@
+// gpsig_amd -- first-order truncated signature kernel Gram on gfx950.
+//
+// Replaces, for order == 1, the dataflow of gpsig/kernels.py:209-238 (_K_seq) +
+// gpsig/signature_algs.py:8-35 (signature_kern_first_order):
+//     dM = second difference of the base-kernel grid M(x_i, y_j)        (signature_algs.py:26)
+//     K_1 = sum dM,  R_m = dM * cumsum_x(cumsum_x(R_{m-1})), K_m = sum R_m   (:28-33)
+// without materialising M or R: one lane group of LP lanes owns one pair (a, b) and streams the
+// rows i of the dM grid; each lane keeps W columns j.  Per row and level the exclusive column
+// prefix S_m(i, j) = sum_{i'<i, j'<j} R_m(i', j') is the exclusive scan over j of the running
+// column sums C_m(j) = sum_{i'<i} R_m(i', j), so per pair the state is (M x W) registers per lane
+// and the only cross-lane traffic is one DPP scan per level per row.  K_m = sum_j C_m(j) at the end.
+//
+#include "sig_fo.h"
+
+namespace gpsig {
+
+// ------------------------------------------------------------------------------------ features
+template <int DP>
+__global__ __launch_bounds__(256) void features_kernel(const float *__restrict__ X, int n, int l, int d,
+                                                       float *__restrict__ F) {
+  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long long)n * l) return;
+  const int i = (int)(idx % l);
+  const float *x = X + idx * d;
+  constexpr int FS = feat_stride(DP);
+  float *f = F + idx * FS;
+  float h = 0.0f;
+#pragma unroll
+  for (int k = 0; k < DP; ++k) {
+    const float xv = k < d ? x[k] : 0.0f;
+    const float dv = (k < d && i + 1 < l) ? x[d + k] - xv : 0.0f;
+    f[k] = xv;
+    f[DP + k] = dv;
+    h = __builtin_fmaf(dv, dv, h);
+  }
+  f[2 * DP] = 0.5f * h;
+#pragma unroll
+  for (int k = 2 * DP + 1; k < FS; ++k) f[k] = 0.0f;
+}
+
+// ------------------------------------------------------------------------------------ launchers
+template <int DP>
+static int launch_features(const float *X, int n, int l, int d, float *F, hipStream_t s) {
+  const long long tot = (long long)n * l;
+  const int blocks = (int)((tot + 255) / 256);
+  hipLaunchKernelGGL(features_kernel<DP>, dim3(blocks), dim3(256), 0, s, X, n, l, d, F);
+  return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
+}
+
+int features(const float *X, int n, int l, int d, int DP, float *F, hipStream_t s) {
+  switch (DP) {
+#define CASE(v) \
+  case v: return launch_features<v>(X, n, l, d, F, s);
+    CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) CASE(16) CASE(32) CASE(64)
+#undef CASE
+    default: return GPSIG_EUNSUPPORTED;
+  }
+}
+
+template <int DP>
+int sig_fo_launch_dp(const SigArgs &a, int seed, long long nblocks, hipStream_t s);
+
+int sig_fo_launch(const SigArgs &a, int DP, int seed, long long nblocks, hipStream_t s) {
+  if (fo_geometry(a.l2).W == 0) return GPSIG_EUNSUPPORTED;
+  switch (DP) {
+#define CASE(v) \
+  case v: return sig_fo_launch_dp<v>(a, seed, nblocks, s);
+    CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(8) CASE(16) CASE(32)
+#undef CASE
+    default: return GPSIG_EUNSUPPORTED;
+  }
+}
+
+int fo_lanes_per_pair(int l2) { return fo_geometry(l2).LP; }
+
+}  // namespace gpsig

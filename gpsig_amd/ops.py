@@ -1,0 +1,216 @@
+"""Typed wrappers over the C ABI (include/gpsig_amd.h) for torch device tensors.
+
+Every function here launches HIP kernels from gpsig_amd/libgpsig_amd.so on the caller's current
+stream; inputs must already be on the GPU (there is no CPU path).  Workspaces are cached per device
+and stream-ordered (a cached buffer is only reused by later launches on the same stream order).
+"""
+from __future__ import annotations
+
+import threading
+
+import torch
+
+from . import _lib as L
+
+_ws_lock = threading.Lock()
+_ws: dict = {}
+
+BASES = {"rbf": L.BASE_RBF, "gauss": L.BASE_RBF, "linear": L.BASE_LINEAR, "lin": L.BASE_LINEAR}
+
+
+def _require_cuda(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise L.GpsigError("gpsig_amd kernels need GPU tensors (device='cuda'); there is no CPU fallback")
+
+
+def _f32(t: torch.Tensor) -> torch.Tensor:
+    return t.to(torch.float32).contiguous() if (t.dtype != torch.float32 or not t.is_contiguous()) else t
+
+
+def _ptr(t):
+    return None if t is None else t.data_ptr()
+
+
+def _stream(device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def workspace(device, nbytes: int) -> torch.Tensor:
+    key = (torch.device(device).index, torch.cuda.current_stream(device).cuda_stream)
+    with _ws_lock:
+        buf = _ws.get(key)
+        if buf is None or buf.numel() < nbytes:
+            buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+            _ws[key] = buf
+        return buf
+
+
+def base_kind(base) -> int:
+    if isinstance(base, int):
+        return base
+    try:
+        return BASES[base.lower()]
+    except KeyError:
+        raise L.GpsigError(f"base kernel {base!r} has no gfx950 kernel (supported: rbf, linear)") from None
+
+
+# ----------------------------------------------------------------------------- truncated kernels
+def sig_diag(X: torch.Tensor, num_levels: int, order: int = 1, base="rbf", difference: bool = True,
+             jitter: float = 0.0, rsqrt: bool = False) -> torch.Tensor:
+    """Per-level k(x_a, x_a), (num_levels+1, n) float32 [rsqrt: 1/sqrt(k + jitter)]."""
+    _require_cuda(X)
+    lib = L.load()
+    X = _f32(X)
+    n, l, d = X.shape
+    out = torch.empty((num_levels + 1, n), dtype=torch.float32, device=X.device)
+    nb = lib.gpsig_sig_workspace_bytes(n, l, n, l, d)
+    ws = workspace(X.device, nb)
+    rc = lib.gpsig_sig_diag(X.data_ptr(), n, l, d, num_levels, order, base_kind(base), int(difference), float(jitter),
+                            L.OUT_RSQRT if rsqrt else L.OUT_LEVELS, out.data_ptr(), ws.data_ptr(), ws.numel(),
+                            _stream(X.device))
+    L.check(rc, "gpsig_sig_diag")
+    return out
+
+
+def sig_gram(X: torch.Tensor, Y: torch.Tensor | None, num_levels: int, order: int = 1, base="rbf",
+             difference: bool = True, rows: tuple | None = None, rs1=None, rs2=None, scale=None,
+             jitter: float = 0.0, out_mode: int = L.OUT_LEVELS, out: torch.Tensor | None = None,
+             out_row0: int | None = None) -> torch.Tensor:
+    """Signature-kernel Gram between the sequences of X (n1,l1,d) and Y (n2,l2,d).
+
+    Y is None -> symmetric K(X): only b >= a is evaluated and mirrored.  rows=(r0, r1) restricts the
+    evaluated rows (row sharding); the output then holds rows [out_row0, out_row0 + out.shape[-2]).
+    out_mode: L.OUT_LEVELS (raw per level), L.OUT_NORM_LEVELS, L.OUT_NORM_SUM (fused normalisation).
+    """
+    _require_cuda(X, Y, rs1, rs2, scale)
+    lib = L.load()
+    X = _f32(X)
+    sym = Y is None
+    Y = X if sym else _f32(Y)
+    n1, l1, d = X.shape
+    n2, l2, d2 = Y.shape
+    if d2 != d:
+        raise ValueError("X and Y must have the same channel count")
+    r0, r1 = (0, n1) if rows is None else rows
+    if out_row0 is None:
+        out_row0 = r0
+    if out is None:
+        nrows = r1 - out_row0
+        shape = (nrows, n2) if out_mode == L.OUT_NORM_SUM else (num_levels + 1, nrows, n2)
+        out = torch.empty(shape, dtype=torch.float32, device=X.device)
+    out_rows = out.shape[-2]
+    if rs1 is not None:
+        rs1, rs2 = _f32(rs1), _f32(rs2)
+    if scale is not None:
+        scale = _f32(scale)
+    nb = lib.gpsig_sig_workspace_bytes(n1, l1, n2, l2, d)
+    ws = workspace(X.device, nb)
+    rc = lib.gpsig_sig_gram(X.data_ptr(), n1, l1, Y.data_ptr(), n2, l2, d, num_levels, order, base_kind(base),
+                            int(difference), L.PAIRS_UPPER if sym else L.PAIRS_RECT, r0, r1,
+                            _ptr(rs1), _ptr(rs2), _ptr(scale), float(jitter), out_mode, out.data_ptr(),
+                            out_row0, out_rows, ws.data_ptr(), ws.numel(), _stream(X.device))
+    L.check(rc, "gpsig_sig_gram")
+    return out
+
+
+# ----------------------------------------------------------------------------- PDE kernel
+def pde_diag(X: torch.Tensor, dyadic: int = 0, solver: int = 1) -> torch.Tensor:
+    _require_cuda(X)
+    lib = L.load()
+    X = _f32(X)
+    n, l, d = X.shape
+    out = torch.empty((n,), dtype=torch.float32, device=X.device)
+    L.check(lib.gpsig_pde_diag(X.data_ptr(), n, l, d, dyadic, solver, out.data_ptr(), _stream(X.device)),
+            "gpsig_pde_diag")
+    return out
+
+
+def pde_gram(X: torch.Tensor, Y: torch.Tensor | None = None, dyadic: int = 0, solver: int = 1,
+             rows: tuple | None = None, out: torch.Tensor | None = None, out_row0: int | None = None) -> torch.Tensor:
+    _require_cuda(X, Y)
+    lib = L.load()
+    X = _f32(X)
+    sym = Y is None
+    Y = X if sym else _f32(Y)
+    n1, l1, d = X.shape
+    n2, l2, _ = Y.shape
+    r0, r1 = (0, n1) if rows is None else rows
+    if out_row0 is None:
+        out_row0 = r0
+    if out is None:
+        out = torch.empty((r1 - out_row0, n2), dtype=torch.float32, device=X.device)
+    rc = lib.gpsig_pde_gram(X.data_ptr(), n1, l1, Y.data_ptr(), n2, l2, d, dyadic, solver,
+                            L.PAIRS_UPPER if sym else L.PAIRS_RECT, r0, r1, out.data_ptr(), out_row0, out.shape[-2],
+                            _stream(X.device))
+    L.check(rc, "gpsig_pde_gram")
+    return out
+
+
+# ----------------------------------------------------------------------------- multi-GPU helper
+def sym_assemble(src: torch.Tensor, row_off: torch.Tensor, level_stride: int, n: int, levels: int,
+                 out: torch.Tensor | None = None) -> torch.Tensor:
+    """Full symmetric (levels, n, n) from gathered UPPER-mode rows: global row a (level 0) starts at
+    element row_off[a] of src, level l at + l*level_stride."""
+    _require_cuda(src, row_off)
+    lib = L.load()
+    if src.dtype != torch.float32 or not src.is_contiguous():
+        raise ValueError("src must be contiguous float32")
+    row_off = row_off.to(torch.int64).contiguous()
+    if out is None:
+        out = torch.empty((levels, n, n), dtype=torch.float32, device=src.device)
+    L.check(lib.gpsig_sym_assemble(src.data_ptr(), row_off.data_ptr(), int(level_stride), n, levels, out.data_ptr(),
+                                   _stream(src.device)), "gpsig_sym_assemble")
+    return out
+
+
+# ----------------------------------------------------------------------------- inducing tensors
+def tens_vs_seq(Z: torch.Tensor, X: torch.Tensor, num_levels: int, order: int = 1, base="rbf",
+                difference: bool = True, increments: bool = False) -> torch.Tensor:
+    """<z_t, S(x_n)> per level: Z (LT,T,D) or (LT,T,2,D) with increments, X (N,L,D) -> (M+1, T, N)."""
+    _require_cuda(Z, X)
+    lib = L.load()
+    Z, X = _f32(Z), _f32(X)
+    lt, t, d = Z.shape[0], Z.shape[1], Z.shape[-1]
+    n, l, dx = X.shape
+    if dx != d:
+        raise ValueError("Z and X must have the same channel count")
+    if lt != num_levels * (num_levels + 1) // 2:
+        raise ValueError(f"Z must have num_levels*(num_levels+1)/2 = {num_levels * (num_levels + 1) // 2} components")
+    out = torch.empty((num_levels + 1, t, n), dtype=torch.float32, device=X.device)
+    ws = workspace(X.device, lib.gpsig_tens_workspace_bytes(n, l, d))
+    rc = lib.gpsig_tens_vs_seq(Z.data_ptr(), lt, t, int(increments), d, X.data_ptr(), n, l, num_levels, order,
+                               base_kind(base), int(difference), out.data_ptr(), ws.data_ptr(), ws.numel(),
+                               _stream(X.device))
+    L.check(rc, "gpsig_tens_vs_seq")
+    return out
+
+
+def tens_gram(Z: torch.Tensor, num_levels: int, base="rbf", increments: bool = False) -> torch.Tensor:
+    """Inducing-tensor Gram per level: Z (LT,T,D) or (LT,T,2,D) -> (M+1, T, T)."""
+    _require_cuda(Z)
+    lib = L.load()
+    Z = _f32(Z)
+    lt, t, d = Z.shape[0], Z.shape[1], Z.shape[-1]
+    out = torch.empty((num_levels + 1, t, t), dtype=torch.float32, device=Z.device)
+    rc = lib.gpsig_tens_gram(Z.data_ptr(), lt, t, int(increments), d, num_levels, base_kind(base), out.data_ptr(),
+                             _stream(Z.device))
+    L.check(rc, "gpsig_tens_gram")
+    return out
+
+
+EMBEDDINGS = {"linear": 0, "rbf": 1}
+
+
+def rescaled(Z: torch.Tensor, X: torch.Tensor, num_levels: int, embedding: str = "linear") -> torch.Tensor:
+    """VOSF <S(x),(I - Lambda_t) S(x)> per level: Z (LT,T,D), X (N,L,D) -> (M+1, N, T)."""
+    _require_cuda(Z, X)
+    lib = L.load()
+    Z, X = _f32(Z), _f32(X)
+    lt, t, d = Z.shape
+    n, l, _ = X.shape
+    out = torch.empty((num_levels + 1, n, t), dtype=torch.float32, device=X.device)
+    rc = lib.gpsig_rescaled(Z.data_ptr(), lt, t, X.data_ptr(), n, l, d, num_levels, EMBEDDINGS[embedding],
+                            out.data_ptr(), _stream(X.device))
+    L.check(rc, "gpsig_rescaled")
+    return out

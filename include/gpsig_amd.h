@@ -1,0 +1,151 @@
+/*
+ * gpsig_amd -- C ABI of the MI355X (gfx950) signature-kernel evaluator.
+ *
+ * Drop-in boundary for the hot path of maudl3116/GPSig (paths relative to the reference root):
+ *   - the per-pair level-M iterated-sums recursion behind SignatureKernel.K/Kdiag/K_tens_vs_seq
+ *       gpsig/kernels.py:190-341 (_K_seq_diag/_K_seq/_K_tens/_K_tens_vs_seq, the algorithm seam)
+ *       gpsig/signature_algs.py:8-160, gpsig/signature_algs_vosf.py:11-48
+ *   - the Goursat-PDE solve behind kernels_pde.UntruncSignatureKernel.Kdiag
+ *       gpsig/sigKer_fast.pyx:15-62 (Cython, OpenMP)
+ *       gpsig/covariance_op/untrunc_cov_op_gpu.cu:5-94 + untrunc_cov_op_gpu.cc:13-150 (CUDA TF op)
+ *
+ * Conventions (all entry points):
+ *   - device pointers, caller-owned buffers, row-major contiguous float32;
+ *   - sequences are (n, l, d): n sequences of l points in R^d (the reference's (N, L*D) input after
+ *     the reshape at gpsig/kernels.py:418-420, with scaling/lags already applied by the host);
+ *   - every call is stream-ordered on `stream` (the caller's current HIP stream), allocates nothing
+ *     (scratch comes from the caller's workspace, sized by the *_workspace_bytes query), performs no
+ *     host synchronisation, and is therefore capturable in a hipGraph;
+ *   - the return value is GPSIG_OK (0) or a negative error code (no exceptions, no aborts).
+ */
+#ifndef GPSIG_AMD_H
+#define GPSIG_AMD_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct ihipStream_t *gpsig_stream_t; /* == hipStream_t */
+
+enum gpsig_status {
+  GPSIG_OK = 0,
+  GPSIG_EINVAL = -1,       /* bad shape / argument */
+  GPSIG_EUNSUPPORTED = -2, /* configuration outside the compiled instantiations */
+  GPSIG_ELAUNCH = -3,      /* HIP launch error (hipGetLastError after the launch) */
+  GPSIG_EWORKSPACE = -4    /* workspace too small */
+};
+
+/* Base (state-space) kernels, gpsig/kernels.py:966-1173. */
+enum gpsig_base_kind {
+  GPSIG_BASE_RBF = 0,    /* SignatureRBF._rbf      kernels.py:1042 : exp(-|x-y|^2/2)  */
+  GPSIG_BASE_LINEAR = 1  /* SignatureLinear._lin   kernels.py:979  : <x, y>           */
+};
+
+/* Which (a, b) sequence pairs a Gram call evaluates. */
+enum gpsig_pair_mode {
+  GPSIG_PAIRS_RECT = 0,  /* all a in [row_begin,row_end) x all b in [0,n2)           (K(X, X2)) */
+  GPSIG_PAIRS_UPPER = 1, /* a in [row_begin,row_end), b in [a, n)  (Y == X, K(X))  + mirrored store */
+  GPSIG_PAIRS_DIAG = 2   /* (a, a) for a in [row_begin,row_end)           (_K_seq_diag) */
+};
+
+/* What a Gram / diag call writes. L = num_levels. */
+enum gpsig_out_mode {
+  GPSIG_OUT_LEVELS = 0,      /* raw per-level values K_m, out (L+1, out_rows, n2) [diag: (L+1, n)] */
+  GPSIG_OUT_NORM_LEVELS = 1, /* scale[m] * (K_m + jit) * rs1[m,a] * rs2[m,b], (L+1, out_rows, n2) */
+  GPSIG_OUT_NORM_SUM = 2,    /* sum over m of the above, (out_rows, n2)                             */
+  GPSIG_OUT_RSQRT = 3        /* diag only: 1/sqrt(K_m(a,a) + jitter), (L+1, n)                      */
+};
+
+/* ---------------------------------------------------------------------------------------------
+ * Truncated signature kernel, seq x seq.
+ *
+ * Replaces _K_seq / _K_seq_diag (kernels.py:190-238) = base kernel tensor (kernels.py:946-1044)
+ * + signature_kern_first_order (signature_algs.py:8-35, order == 1) or
+ * signature_kern_higher_order (signature_algs.py:37-74, order > 1), with the normalisation and
+ * sigma*variances epilogue of SignatureKernel.K (kernels.py:431-477) fused in (out_mode 1/2).
+ *
+ *   X (n1, l1, d), Y (n2, l2, d); for GPSIG_PAIRS_UPPER / DIAG pass Y == X (n2 == n1, l2 == l1).
+ *   order: 1 = first order; >1 = higher order (clamped by the caller as kernels.py:58 does).
+ *   difference: kernels.py `difference` flag (second-difference the base-kernel grid).
+ *   rs1 (L+1, n1), rs2 (L+1, n2): 1/sqrt(diag + jitter) from gpsig_sig_diag(GPSIG_OUT_RSQRT), or
+ *     NULL for "no normalisation".  scale (L+1): sigma * variances (NULL = ones).
+ *   jitter: added to K_m(a,a) before normalising in GPSIG_PAIRS_UPPER (kernels.py:432).
+ *   out rows are a - out_row0 for a in [out_row0, out_row0 + out_rows); in UPPER mode the mirrored
+ *     entry (b, a) is also stored when b lies in that row window.
+ */
+size_t gpsig_sig_workspace_bytes(int n1, int l1, int n2, int l2, int d);
+
+int gpsig_sig_gram(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int num_levels,
+                   int order, int base_kind, int difference, int pair_mode, int row_begin, int row_end,
+                   const float *rs1, const float *rs2, const float *scale, float jitter, int out_mode,
+                   float *out, int out_row0, int out_rows, void *workspace, size_t workspace_bytes,
+                   gpsig_stream_t stream);
+
+/* Diagonal k(x_a, x_a) per level: _K_seq_diag (kernels.py:190-207).  out_mode LEVELS or RSQRT. */
+int gpsig_sig_diag(const float *X, int n, int l, int d, int num_levels, int order, int base_kind, int difference,
+                   float jitter, int out_mode, float *out, void *workspace, size_t workspace_bytes,
+                   gpsig_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Inducing tensors (sparse rank-1 tensors z = (z_{m,1} (x) ... (x) z_{m,m})_m).
+ *
+ * gpsig_tens_vs_seq replaces _K_tens_vs_seq (kernels.py:314-341) = base kernel between tensor
+ * components and sequence points + signature_kern_tens_vs_seq_first_order / _higher_order
+ * (signature_algs.py:101-160).  Z (LT, T, d), or (LT, T, 2, d) with increments (kernels.py:328-331),
+ * LT = num_levels (num_levels+1) / 2; X (n, l, d).  out (num_levels+1, T, n), raw (unnormalised).
+ *
+ * gpsig_tens_gram replaces _K_tens (kernels.py:264-284) + tensor_kern (signature_algs.py:76-99):
+ * out (num_levels+1, T, T).
+ *
+ * gpsig_rescaled replaces _Mahalanobis_term_approx_posterior (kernels.py:800-822, linear embedding
+ * = 0; kernels_pde.py:191-222, per-coordinate RBF embedding = 1) + signature_kern_rescaled_higher_order
+ * (signature_algs_vosf.py:11-48): <S(x_n), (I - Lambda_t) S(x_n)> per level with Lambda_t the rank-1
+ * diagonal built from Z (LT, T, d).  out (num_levels+1, n, T).
+ */
+size_t gpsig_tens_workspace_bytes(int n, int l, int d);
+
+int gpsig_tens_vs_seq(const float *Z, int lt, int t, int increments, int d, const float *X, int n, int l,
+                      int num_levels, int order, int base_kind, int difference, float *out, void *workspace,
+                      size_t workspace_bytes, gpsig_stream_t stream);
+
+int gpsig_tens_gram(const float *Z, int lt, int t, int increments, int d, int num_levels, int base_kind, float *out,
+                    gpsig_stream_t stream);
+
+int gpsig_rescaled(const float *Z, int lt, int t, const float *X, int n, int l, int d, int num_levels,
+                   int embedding, float *out, gpsig_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Goursat PDE (untruncated signature kernel).
+ *
+ * Replaces sig_kern_diag (sigKer_fast.pyx:15-62) and the UntruncCov op
+ * (untrunc_cov_op_gpu.cc:13-25 -> UntruncCovKernelLauncher, untrunc_cov_op_gpu.cu:71-81), which
+ * solve k(x, x) only; gpsig_pde_gram adds the cross Gram the reference lacks (kernels_pde.py:107
+ * calls an undefined K).  dyadic = the reference `order`/`n` (grid refined 2^dyadic per increment),
+ * solver 1 = explicit scheme (sigKer_fast.pyx:48 / .cu:29), 0 = first-order scheme (:46).
+ * out: final corner K[-1,-1] per pair (kernels_pde.py:185 takes K_diag[:, -1, -1]).
+ */
+int gpsig_pde_gram(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int dyadic, int solver,
+                   int pair_mode, int row_begin, int row_end, float *out, int out_row0, int out_rows,
+                   gpsig_stream_t stream);
+
+int gpsig_pde_diag(const float *X, int n, int l, int d, int dyadic, int solver, float *out, gpsig_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Multi-GPU assembly helper (no reference counterpart: the reference has no distributed code).
+ * After an all-gather of UPPER-mode row blocks, build the full symmetric matrix:
+ *   dst[l][a][b] = src[row_off[a] + l*level_stride + b]   for b >= a,
+ *                  src[row_off[b] + l*level_stride + a]   otherwise;   dst (levels, n, n).
+ * row_off (n): element offset of global row a (level 0) inside the gathered buffer.
+ */
+int gpsig_sym_assemble(const float *src, const long long *row_off, long long level_stride, int n, int levels,
+                       float *dst, gpsig_stream_t stream);
+
+/* Library identification (for tests: the loaded object must be this build). */
+const char *gpsig_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* GPSIG_AMD_H */

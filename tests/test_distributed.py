@@ -1,0 +1,108 @@
+"""CPU, world_size 2 (gloo): the row-sharding partition, the all-gather layout and the symmetric
+assembly of gpsig_amd.distributed reproduce the single-process Gram.  The per-rank compute is the
+float64 oracle (stand-in for the GPU kernel, which needs a GPU) and the assembly is a torch
+restatement of gpsig_sym_assemble; the GPU kernel itself is covered in test_gram_gpu.py."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from gpsig_amd import distributed as D
+from gpsig_amd import _lib as L
+from oracle import kernels_ref as kr
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _oracle_levels(X, M):
+    k = kr.SignatureKernelRef(X.shape[1] * X.shape[2], X.shape[2], M, normalization=False)
+    return torch.as_tensor(k.K_seq(X.numpy().astype(np.float64)), dtype=torch.float32)
+
+
+def _compute_sym(X, levels, rows, out, out_row0, num_levels, out_mode, full=None, **kw):
+    """UPPER-mode semantics of gpsig_sig_gram: rows [r0,r1), pairs b >= a, mirrored inside the window."""
+    r0, r1 = rows
+    n = X.shape[0]
+    for a in range(r0, r1):
+        for b in range(a, n):
+            v = full[:, a, b] if out_mode != L.OUT_NORM_SUM else full[:, a, b].sum(0, keepdim=True)
+            out[:, a - out_row0, b] = v
+            if out_row0 <= b < out_row0 + out.shape[1]:
+                out[:, b - out_row0, a] = v
+
+
+def _assemble_torch(gathered, row_off, level_stride, n, levels):
+    flat = gathered.reshape(-1)
+    out = torch.empty((levels, n, n))
+    for l in range(levels):
+        for a in range(n):
+            for b in range(n):
+                r, c = (a, b) if b >= a else (b, a)
+                out[l, a, b] = flat[row_off[r] + l * level_stride + c]
+    return out
+
+
+def _worker(rank, world, port, n, M, mode, q):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(0)
+    X = torch.as_tensor(np.cumsum(rng.standard_normal((n, 12, 2)), 1) * 0.2, dtype=torch.float32)
+    full = _oracle_levels(X, M)
+    res = D.sharded_sym_gram(X, M, out_mode=mode, compute=lambda *a, **k: _compute_sym(*a, full=full, **k),
+                             assemble=_assemble_torch)
+    q.put((rank, res.numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n", [13, 24])
+@pytest.mark.parametrize("mode", [L.OUT_NORM_SUM, L.OUT_NORM_LEVELS])
+def test_sharded_symmetric_gram_world2(n, mode):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    M = 3
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, n, M, mode, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    rng = np.random.default_rng(0)
+    X = torch.as_tensor(np.cumsum(rng.standard_normal((n, 12, 2)), 1) * 0.2, dtype=torch.float32)
+    full = _oracle_levels(X, M).numpy()
+    exp = full.sum(0) if mode == L.OUT_NORM_SUM else full
+    for r in (0, 1):
+        np.testing.assert_allclose(res[r], exp, rtol=1e-6, atol=1e-7)
+
+
+def test_triangle_partition_balanced():
+    for n, world in [(4096, 8), (4096, 2), (8192, 8), (100, 4)]:
+        chunks, B = D.triangle_chunks(n, world)
+        covered = sorted(r for s, e in chunks for r in range(s, e))
+        assert covered == list(range(n))
+        work = []
+        for rank in range(world):
+            (a0, a1), (b0, b1), _ = D.rank_chunks(n, world, rank)
+            work.append(sum(n - a for a in range(a0, a1)) + sum(n - a for a in range(b0, b1)))
+        assert max(work) / (sum(work) / world) < 1.06, work
+
+
+def test_row_offsets_layout():
+    n, world, levels = 50, 4, 3
+    chunks, B = D.triangle_chunks(n, world)
+    off = D.row_offsets(n, world, levels)
+    # every row maps to a distinct B*n-aligned slot inside (world, 2, levels, B, n)
+    slots = sorted(int(o) // n for o in off)
+    assert len(set(slots)) == n and max(off) < world * 2 * levels * B * n

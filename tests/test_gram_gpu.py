@@ -1,0 +1,171 @@
+"""GPU parity: the gfx950 truncated-signature kernels vs the float64 oracle / golden fixtures.
+
+Criterion (BASELINE.json north_star "within 1e-5 relative fp32"): norm-relative
+max|K32 - K64| <= TOL * max|K64|, per level and for the summed normalised Gram.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden, norm_rel_err
+from oracle import kernels_ref as kr
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+DEV = "cuda"
+
+
+def t(x):
+    return torch.as_tensor(np.asarray(x), device=DEV)
+
+
+def test_rbf_gram_matches_fixture():
+    import gpsig_amd
+    g = golden("rbf_gram.npz")
+    X, X2, M = g["X"], g["X2"], int(g["num_levels"])
+    N, L, D = X.shape
+    k = gpsig_amd.SignatureRBF(L * D, D, M)
+    K = k.K(t(X.reshape(N, -1))).cpu().numpy()
+    assert norm_rel_err(K, g["K"]) < TOL
+    Kl = k.K(t(X.reshape(N, -1)), return_levels=True).cpu().numpy()
+    assert (norm_rel_err(Kl[1:], g["K_levels"][1:], axis_levels=True) < TOL).all()
+    Kc = k.K(t(X.reshape(N, -1)), t(X2.reshape(len(X2), -1)), return_levels=True).cpu().numpy()
+    assert (norm_rel_err(Kc, g["K_cross_levels"], axis_levels=True) < TOL).all()
+    # float64 in -> float64 out (drop-in dtype), symmetric, unit diagonal per level
+    assert k.K(t(X.reshape(N, -1))).dtype == torch.float64
+    np.testing.assert_allclose(K, K.T, atol=1e-6)
+    for m in range(M + 1):
+        np.testing.assert_allclose(np.diag(Kl[m]), 1.0, atol=2e-6)
+
+
+def test_rbf_raw_levels_and_diag():
+    import gpsig_amd
+    from gpsig_amd import ops
+    g = golden("rbf_gram.npz")
+    X, M = g["X"], int(g["num_levels"])
+    raw = ops.sig_gram(t(X), None, M).cpu().numpy()
+    err = norm_rel_err(raw[1:], g["K_raw"][1:], axis_levels=True)
+    assert (err < TOL).all(), err
+    d = ops.sig_diag(t(X), M).cpu().numpy()
+    assert (norm_rel_err(d[1:], g["Kdiag_raw"][1:], axis_levels=True) < TOL).all()
+    k = gpsig_amd.SignatureRBF(X.shape[1] * X.shape[2], X.shape[2], M, normalization=False)
+    assert norm_rel_err(k.Kdiag(t(X.reshape(len(X), -1))).cpu().numpy(), g["Kdiag_unnorm"]) < TOL
+    kn = gpsig_amd.SignatureRBF(X.shape[1] * X.shape[2], X.shape[2], M)
+    np.testing.assert_allclose(kn.Kdiag(t(X.reshape(len(X), -1))).cpu().numpy(), g["Kdiag_norm"])
+
+
+def test_rbf_rough_data_with_lengthscales_and_variances():
+    import gpsig_amd
+    g = golden("rbf_rough.npz")
+    X, M = g["X"], int(g["num_levels"])
+    N, L, D = X.shape
+    k = gpsig_amd.SignatureRBF(L * D, D, M, lengthscales=g["lengthscales"], variances=g["variances"])
+    Kl = k.K(t(X.reshape(N, -1)), return_levels=True).cpu().numpy()
+    assert (norm_rel_err(Kl, g["K_levels"], axis_levels=True) < TOL).all()
+
+
+def test_linear_order_M_matches_chen_signatures():
+    """esig-equivalent check (reference notebooks/signature_kernel.ipynb:52-140, 2.24e-8 in fp64)."""
+    import gpsig_amd
+    g = golden("linear_chen.npz")
+    X, M = g["X"], int(g["num_levels"])
+    N, L, D = X.shape
+    k = gpsig_amd.SignatureLinear(L * D, D, M, order=M, normalization=False)
+    Kl = k.K(t(X.reshape(N, -1)), return_levels=True).cpu().numpy()
+    err = norm_rel_err(Kl, g["K_chen"], axis_levels=True)
+    assert (err < TOL).all(), err
+
+
+@pytest.mark.parametrize("order", [2, 3, 4])
+@pytest.mark.parametrize("base", ["rbf", "lin"])
+def test_higher_order(order, base):
+    from gpsig_amd import ops
+    g = golden("higher_order.npz")
+    X, M = g["X"], int(g["num_levels"])
+    got = ops.sig_gram(t(X), None, M, order=order, base="rbf" if base == "rbf" else "linear").cpu().numpy()
+    err = norm_rel_err(got[1:], g[f"{base}_order{order}"][1:], axis_levels=True)
+    assert (err < TOL).all(), err
+
+
+@pytest.mark.parametrize("nl", [1, 2])
+def test_lags(nl):
+    import gpsig_amd
+    g = golden("lags.npz")
+    X, M = g["X"], int(g["num_levels"])
+    N, L, D = X.shape
+    k = gpsig_amd.SignatureRBF(L * D, D, M, num_lags=nl)
+    Kl = k.K(t(X.reshape(N, -1)), return_levels=True).cpu().numpy()
+    assert (norm_rel_err(Kl, g[f"lags{nl}_K_levels"], axis_levels=True) < TOL).all()
+
+
+@pytest.mark.parametrize("base", ["rbf", "linear"])
+def test_no_difference(base):
+    from gpsig_amd import ops
+    g = golden("nodiff.npz")
+    X, M = g["X"], int(g["num_levels"])
+    got = ops.sig_gram(t(X), None, M, base=base, difference=False).cpu().numpy()
+    assert (norm_rel_err(got[1:], g[f"{base}_nodiff"][1:], axis_levels=True) < TOL).all()
+
+
+@pytest.mark.parametrize("L", [2, 3, 17, 33, 64, 65, 128, 129, 200, 257, 300])
+def test_lengths_and_geometries(L):
+    """Every lane-geometry branch (LP=16/32/64, W=4/8) incl. ragged edges, vs the oracle."""
+    from gpsig_amd import ops
+    rng = np.random.default_rng(L)
+    N1, N2, D, M = 5, 3, 4, 4
+    X = np.cumsum(rng.standard_normal((N1, L, D)), 1) / np.sqrt(L * D)
+    Y = np.cumsum(rng.standard_normal((N2, max(L - 1, 2), D)), 1) / np.sqrt(L * D)
+    ref = kr.SignatureKernelRef(L * D, D, M, normalization=False)
+    exp = ref.K_seq(X, Y)
+    got = ops.sig_gram(t(X), t(Y), M).cpu().numpy()
+    assert (norm_rel_err(got[1:], exp[1:], axis_levels=True) < TOL).all()
+    sym = ops.sig_gram(t(X), None, M).cpu().numpy()
+    exps = ref.K_seq(X)
+    assert (norm_rel_err(sym[1:], exps[1:], axis_levels=True) < TOL).all()
+
+
+@pytest.mark.parametrize("D", [1, 2, 3, 5, 6, 7, 8, 11, 16, 20])
+@pytest.mark.parametrize("M", [1, 2, 6, 8])
+def test_channels_and_levels(D, M):
+    from gpsig_amd import ops
+    rng = np.random.default_rng(100 * D + M)
+    X = np.cumsum(rng.standard_normal((6, 24, D)), 1) / np.sqrt(24 * D)
+    exp = kr.SignatureKernelRef(24 * D, D, M, normalization=False).K_seq(X)
+    got = ops.sig_gram(t(X), None, M).cpu().numpy()
+    assert (norm_rel_err(got[1:], exp[1:], axis_levels=True) < TOL).all()
+
+
+def test_row_windows_and_rect_tiles():
+    """Row sharding windows: (rows, out_row0) of both pair modes reproduce the full Gram."""
+    from gpsig_amd import ops
+    import gpsig_amd._lib as L
+    rng = np.random.default_rng(5)
+    X = torch.as_tensor(np.cumsum(rng.standard_normal((37, 30, 3)), 1) / 10, device=DEV, dtype=torch.float32)
+    full = ops.sig_gram(X, None, 4)
+    for r0, r1 in [(0, 9), (9, 21), (21, 37), (3, 4)]:
+        part = ops.sig_gram(X, X, 4, rows=(r0, r1))
+        torch.testing.assert_close(part, full[:, r0:r1], rtol=1e-5, atol=1e-6)
+        up = torch.zeros(5, r1 - r0, 37, device=DEV)
+        ops.sig_gram(X, None, 4, rows=(r0, r1), out=up)
+        mask = torch.arange(37, device=DEV)[None, :] >= torch.arange(r0, r1, device=DEV)[:, None]
+        torch.testing.assert_close(up[:, mask], full[:, r0:r1][:, mask], rtol=1e-5, atol=1e-6)
+
+
+def test_full_size_properties_headline():
+    """At the headline sequence shape (L=128, D=5, M=5): a 256-row subsample vs the oracle, plus
+    size-independent properties of the full normalised Gram (symmetry, unit diagonal, PSD)."""
+    import gpsig_amd
+    rng = np.random.default_rng(0)
+    N, L, D, M = 512, 128, 5, 5
+    X = np.cumsum(rng.standard_normal((N, L, D)), 1) / np.sqrt(L * D)
+    k = gpsig_amd.SignatureRBF(L * D, D, M)
+    Xt = torch.as_tensor(X.reshape(N, -1), device=DEV, dtype=torch.float32)
+    K = k.K(Xt).double()
+    torch.testing.assert_close(K, K.T, rtol=0, atol=1e-6)
+    torch.testing.assert_close(torch.diagonal(K), torch.full((N,), 6.0, dtype=K.dtype, device=DEV), rtol=0, atol=1e-5)
+    assert torch.linalg.eigvalsh(K).min().item() > -1e-4
+    idx = np.arange(0, N, 64)
+    ref = kr.SignatureKernelRef(L * D, D, M)
+    exp = ref.K(X[idx].reshape(len(idx), -1), X[:40].reshape(40, -1))
+    got = k.K(Xt[idx], Xt[:40]).cpu().numpy()
+    assert norm_rel_err(got, exp) < TOL
