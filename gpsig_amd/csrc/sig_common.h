@@ -70,13 +70,19 @@ template <int DP, int W, int SEED>
 struct RowSeed {
   static constexpr int FS = feat_stride(DP);
   static constexpr bool DIFF = (SEED == SEED_RBF_DIFF || SEED == SEED_LIN_DIFF);
+  static constexpr int ANCHOR = 8;  // exact |x_i - y_j|^2 every ANCHOR rows (d^2 row recurrence between)
+  static constexpr float NHL2E = -0.72134752044448170f;  // -log2(e)/2: exp(-d2/2) = exp2(d2 * NHL2E)
   float y[W][DP], dy[W][DP], hdy[W];
-  bool valid[W];
-  // RBF_DIFF row state
-  float diff[W][DP], kc[W], kcR;
+  bool valid_last;  // column W-1 of this lane is a real cell (others: exact zeros by construction)
+  bool valid[W];    // POINT seeds
+  // RBF_DIFF row state: diff = x_i - y_j, d2 = |diff|^2, kc = k(x_i, y_j), kcR = next lane's kc[0]
+  float diff[W][DP], d2[W], kc[W], kcR;
 
   GPSIG_DEV void init(const float *__restrict__ fx, const float *__restrict__ fy, int gl, int l2) {
     const int ncols = DIFF ? l2 - 1 : l2;
+    // Points beyond the sequence are clamped to its last point, whose increment record is zero, so
+    // every DIFF-seed cell of a padded column evaluates to exactly 0 (both the stable and the corner
+    // form); only the lane's last column can see a foreign right neighbour and is masked.
 #pragma unroll
     for (int w = 0; w < W; ++w) {
       const int j = gl * W + w;
@@ -90,6 +96,7 @@ struct RowSeed {
       }
       hdy[w] = f[2 * DP];
     }
+    valid_last = valid[W - 1];
     if constexpr (SEED == SEED_RBF_DIFF) {
 #pragma unroll
       for (int w = 0; w < W; ++w) {
@@ -99,52 +106,62 @@ struct RowSeed {
           diff[w][k] = fx[k] - y[w][k];
           s = __builtin_fmaf(diff[w][k], diff[w][k], s);
         }
-        kc[w] = fast_exp(-0.5f * s);
+        d2[w] = s;
+        kc[w] = __builtin_amdgcn_exp2f(s * NHL2E);
       }
       kcR = lane_next(kc[0]);
     }
   }
 
+  // Cells of row i.  rd = wave-uniform record of row i (x_{i+1} for RBF DIFF, x_i for POINT seeds).
+  // ANCH: re-evaluate |x_{i+1} - y_j|^2 exactly instead of the d2 - 2p recurrence.
+  template <bool ANCH>
   GPSIG_DEV void row(const RowData<DP> &rd, float (&dM)[W]) {
     if constexpr (SEED == SEED_RBF_DIFF) {
-      float kn[W], diffn[W][DP];
+      // 1) p, q, c from the current diff = x_i - y_j (consumed before diff is overwritten)
+      float pp[W], q[W], c[W];
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        float a = -rd.hdx, bq = -hdy[w], cc = 0.0f;
+#pragma unroll
+        for (int k = 0; k < DP; ++k) {
+          a = __builtin_fmaf(-diff[w][k], rd.dx[k], a);
+          bq = __builtin_fmaf(diff[w][k], dy[w][k], bq);
+          cc = __builtin_fmaf(rd.dx[k], dy[w][k], cc);
+        }
+        pp[w] = a;
+        q[w] = bq;
+        c[w] = cc;
+      }
+      // 2) next row: diff = x_{i+1} - y_j, |diff|^2 = d2 - 2p (exact re-anchor every ANCHOR rows)
+      float kn[W];
 #pragma unroll
       for (int w = 0; w < W; ++w) {
         float s = 0.0f;
 #pragma unroll
         for (int k = 0; k < DP; ++k) {
-          diffn[w][k] = rd.x[k] - y[w][k];
-          s = __builtin_fmaf(diffn[w][k], diffn[w][k], s);
+          diff[w][k] = rd.x[k] - y[w][k];
+          if constexpr (ANCH) s = __builtin_fmaf(diff[w][k], diff[w][k], s);
         }
-        kn[w] = fast_exp(-0.5f * s);
+        d2[w] = ANCH ? s : __builtin_fmaf(-2.0f, pp[w], d2[w]);
+        kn[w] = __builtin_amdgcn_exp2f(d2[w] * NHL2E);
       }
       const float knR = lane_next(kn[0]);
+      // 3) the cells
 #pragma unroll
       for (int w = 0; w < W; ++w) {
-        float pp = -rd.hdx, q = -hdy[w], c = 0.0f;
-#pragma unroll
-        for (int k = 0; k < DP; ++k) {
-          const float dxk = rd.dx[k];
-          pp = __builtin_fmaf(-diff[w][k], dxk, pp);
-          q = __builtin_fmaf(diff[w][k], dy[w][k], q);
-          c = __builtin_fmaf(dxk, dy[w][k], c);
-        }
         const float kn1 = (w + 1 < W) ? kn[w + 1] : knR;
         const float kc1 = (w + 1 < W) ? kc[w + 1] : kcR;
         const float naive = (kn1 - kn[w]) - (kc1 - kc[w]);
-        const float Ep = em1_small(pp), Eq = em1_small(q), Ec = em1_small(c);
+        const float Ep = em1_small(pp[w]), Eq = em1_small(q[w]), Ec = em1_small(c[w]);
         const float stable = kc[w] * __builtin_fmaf(Ep, Eq, (1.0f + Ep) * (1.0f + Eq) * Ec);
-        const bool small = __builtin_fabsf(pp) < EM1_TAU && __builtin_fabsf(q) < EM1_TAU &&
-                           __builtin_fabsf(c) < EM1_TAU;
-        const float v = small ? stable : naive;
-        dM[w] = valid[w] ? v : 0.0f;
+        const float mx = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(pp[w]), __builtin_fabsf(q[w])),
+                                         __builtin_fabsf(c[w]));
+        const float v = mx < EM1_TAU ? stable : naive;
+        dM[w] = (w + 1 < W || valid_last) ? v : 0.0f;
       }
 #pragma unroll
-      for (int w = 0; w < W; ++w) {
-        kc[w] = kn[w];
-#pragma unroll
-        for (int k = 0; k < DP; ++k) diff[w][k] = diffn[w][k];
-      }
+      for (int w = 0; w < W; ++w) kc[w] = kn[w];
       kcR = knR;
     } else if constexpr (SEED == SEED_LIN_DIFF) {
 #pragma unroll
@@ -152,7 +169,7 @@ struct RowSeed {
         float c = 0.0f;
 #pragma unroll
         for (int k = 0; k < DP; ++k) c = __builtin_fmaf(rd.dx[k], dy[w][k], c);
-        dM[w] = valid[w] ? c : 0.0f;
+        dM[w] = c;  // padded columns have dy == 0
       }
     } else if constexpr (SEED == SEED_RBF_POINT) {
 #pragma unroll
@@ -163,7 +180,7 @@ struct RowSeed {
           const float t = rd.x[k] - y[w][k];
           s = __builtin_fmaf(t, t, s);
         }
-        dM[w] = valid[w] ? fast_exp(-0.5f * s) : 0.0f;
+        dM[w] = valid[w] ? __builtin_amdgcn_exp2f(s * NHL2E) : 0.0f;
       }
     } else {
 #pragma unroll

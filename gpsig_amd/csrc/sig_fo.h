@@ -12,11 +12,15 @@
 // they interleave).  K_m = sum_j C_m(j) at the end.  The seed (base-kernel second difference,
 // including the fp32-stable RBF form) is RowSeed in sig_common.h.
 #pragma once
+#include <type_traits>
+
 #include "sig_common.h"
 
 namespace gpsig {
 
-template <int DP, int W, int LP, int M, int SEED>
+// DIAGK: the diagonal pass (pairs (a, a)) is the same body under its own symbol, so profiler
+// statistics of the Gram launch are not mixed with it.
+template <int DP, int W, int LP, int M, int SEED, bool DIAGK>
 __global__ __launch_bounds__(256) void sig_fo_kernel(SigArgs p) {
   using Seed = RowSeed<DP, W, SEED>;
   constexpr int FS = feat_stride(DP);
@@ -29,7 +33,7 @@ __global__ __launch_bounds__(256) void sig_fo_kernel(SigArgs p) {
 
   // ---- which pair
   int a, b;
-  if (p.pair_mode == GPSIG_PAIRS_DIAG) {
+  if (DIAGK) {
     a = p.row_begin + (int)blockIdx.x * 4 + wave;
     b = a;
     if (a >= p.row_end) return;
@@ -49,7 +53,7 @@ __global__ __launch_bounds__(256) void sig_fo_kernel(SigArgs p) {
   }
   bool pair_ok = b < p.n2;
   if (p.pair_mode == GPSIG_PAIRS_UPPER) pair_ok = pair_ok && b >= a;
-  if (p.pair_mode == GPSIG_PAIRS_DIAG) pair_ok = (g == 0);
+  if (DIAGK) pair_ok = (g == 0);
   const int bl = b < p.n2 ? b : p.n2 - 1;
 
   const float *__restrict__ fx = p.FX + (long long)a * p.l1 * FS;
@@ -65,17 +69,11 @@ __global__ __launch_bounds__(256) void sig_fo_kernel(SigArgs p) {
     for (int w = 0; w < W; ++w) C[m][w] = 0.0f;
 
   const int nrows = Seed::DIFF ? p.l1 - 1 : p.l1;
-  RowData<DP> rd;
-  rd.load(fx, 0, SEED);
-  for (int i = 0; i < nrows; ++i) {
-    // prefetch the next row's wave-uniform record (scalar loads) so their latency hides here
-    RowData<DP> rn;
-    rn.load(fx, i + 1 < nrows ? i + 1 : i, SEED);
-
+  // One row: seed cells, then the level recursion.  S_m = exclusive prefix over (rows < i, cols < j)
+  // of R_m = exclusive scan over j of C_m; the M-1 scans are independent and interleave.
+  auto do_row = [&](const RowData<DP> &rd, auto anch) {
     float dM[W];
-    seed.row(rd, dM);
-
-    // ---- level recursion: S_m = exclusive prefix over (rows < i, cols < j) of R_m
+    seed.template row<decltype(anch)::value>(rd, dM);
     float S[M > 1 ? M - 1 : 1][W];
 #pragma unroll
     for (int m = 0; m + 1 < M; ++m) {
@@ -95,7 +93,36 @@ __global__ __launch_bounds__(256) void sig_fo_kernel(SigArgs p) {
     for (int m = 0; m + 1 < M; ++m)
 #pragma unroll
       for (int w = 0; w < W; ++w) C[m + 1][w] = __builtin_fmaf(dM[w], S[m][w], C[m + 1][w]);
-    rd = rn;
+  };
+  if constexpr (SEED == SEED_RBF_DIFF && !DIAGK && DP <= 8) {
+    // Blocks of ANCHOR rows, fully unrolled (no register rotation at the back edge); the block's
+    // last row re-anchors |x - y|^2.  The row records are wave-uniform scalar loads, hoisted.
+    constexpr int BLK = Seed::ANCHOR;
+    int i = 0;
+    for (; i + BLK <= nrows; i += BLK) {
+      RowData<DP> rd[BLK];
+#pragma unroll
+      for (int u = 0; u < BLK; ++u) rd[u].load(fx, i + u, SEED);
+#pragma unroll
+      for (int u = 0; u < BLK; ++u) {
+        if (u + 1 < BLK)
+          do_row(rd[u], std::false_type{});
+        else
+          do_row(rd[u], std::true_type{});
+      }
+    }
+    for (; i < nrows; ++i) {
+      RowData<DP> rd;
+      rd.load(fx, i, SEED);
+      do_row(rd, std::true_type{});
+    }
+  } else {
+    // plain row loop (diagonal pass, cheap seeds); RBF distances evaluated exactly every row
+    for (int i = 0; i < nrows; ++i) {
+      RowData<DP> rd;
+      rd.load(fx, i, SEED);
+      do_row(rd, std::true_type{});
+    }
   }
 
   // ---- epilogue: K_m = sum_j C_m(j)
@@ -125,7 +152,10 @@ constexpr int FO_MAX_LEVELS = 8;
 template <int DP, int W, int LP, int M, int SEED>
 int launch_fo(const SigArgs &a, long long nblocks, hipStream_t s) {
   if (nblocks <= 0) return GPSIG_OK;
-  hipLaunchKernelGGL((sig_fo_kernel<DP, W, LP, M, SEED>), dim3((unsigned)nblocks), dim3(256), 0, s, a);
+  if (a.pair_mode == GPSIG_PAIRS_DIAG)
+    hipLaunchKernelGGL((sig_fo_kernel<DP, W, LP, M, SEED, true>), dim3((unsigned)nblocks), dim3(256), 0, s, a);
+  else
+    hipLaunchKernelGGL((sig_fo_kernel<DP, W, LP, M, SEED, false>), dim3((unsigned)nblocks), dim3(256), 0, s, a);
   return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
 }
 
@@ -139,30 +169,15 @@ int fo_geo(const SigArgs &a, long long nblocks, hipStream_t s) {
   return GPSIG_EUNSUPPORTED;
 }
 
-template <int DP, int SEED>
-int fo_levels(const SigArgs &a, long long nblocks, hipStream_t s) {
-  switch (a.M) {
-    case 1: return fo_geo<DP, 1, SEED>(a, nblocks, s);
-    case 2: return fo_geo<DP, 2, SEED>(a, nblocks, s);
-    case 3: return fo_geo<DP, 3, SEED>(a, nblocks, s);
-    case 4: return fo_geo<DP, 4, SEED>(a, nblocks, s);
-    case 5: return fo_geo<DP, 5, SEED>(a, nblocks, s);
-    case 6: return fo_geo<DP, 6, SEED>(a, nblocks, s);
-    case 7: return fo_geo<DP, 7, SEED>(a, nblocks, s);
-    case 8: return fo_geo<DP, 8, SEED>(a, nblocks, s);
-    default: return GPSIG_EUNSUPPORTED;
-  }
-}
-
-// One explicit instantiation per channel count lives in its own translation unit
-// (sig_fo_inst.hip compiled with -DGPSIG_DP=...), so the instantiations build in parallel.
-template <int DP>
-int sig_fo_launch_dp(const SigArgs &a, int seed, long long nblocks, hipStream_t s) {
+// One explicit instantiation per (channel count, level count) lives in its own translation unit
+// (sig_fo_inst.hip compiled with -DGPSIG_DP=.. -DGPSIG_M=..), so the instantiations build in parallel.
+template <int DP, int M>
+int sig_fo_launch_dpm(const SigArgs &a, int seed, long long nblocks, hipStream_t s) {
   switch (seed) {
-    case SEED_RBF_DIFF: return fo_levels<DP, SEED_RBF_DIFF>(a, nblocks, s);
-    case SEED_LIN_DIFF: return fo_levels<DP, SEED_LIN_DIFF>(a, nblocks, s);
-    case SEED_RBF_POINT: return fo_levels<DP, SEED_RBF_POINT>(a, nblocks, s);
-    case SEED_LIN_POINT: return fo_levels<DP, SEED_LIN_POINT>(a, nblocks, s);
+    case SEED_RBF_DIFF: return fo_geo<DP, M, SEED_RBF_DIFF>(a, nblocks, s);
+    case SEED_LIN_DIFF: return fo_geo<DP, M, SEED_LIN_DIFF>(a, nblocks, s);
+    case SEED_RBF_POINT: return fo_geo<DP, M, SEED_RBF_POINT>(a, nblocks, s);
+    case SEED_LIN_POINT: return fo_geo<DP, M, SEED_LIN_POINT>(a, nblocks, s);
     default: return GPSIG_EUNSUPPORTED;
   }
 }

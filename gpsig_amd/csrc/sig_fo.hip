@@ -57,14 +57,29 @@ int features(const float *X, int n, int l, int d, int DP, float *F, hipStream_t 
   }
 }
 
+template <int DP, int M>
+int sig_fo_launch_dpm(const SigArgs &a, int seed, long long nblocks, hipStream_t s);
+
 template <int DP>
-int sig_fo_launch_dp(const SigArgs &a, int seed, long long nblocks, hipStream_t s);
+static int fo_dp(const SigArgs &a, int seed, long long nblocks, hipStream_t s) {
+  switch (a.M) {
+    case 1: return sig_fo_launch_dpm<DP, 1>(a, seed, nblocks, s);
+    case 2: return sig_fo_launch_dpm<DP, 2>(a, seed, nblocks, s);
+    case 3: return sig_fo_launch_dpm<DP, 3>(a, seed, nblocks, s);
+    case 4: return sig_fo_launch_dpm<DP, 4>(a, seed, nblocks, s);
+    case 5: return sig_fo_launch_dpm<DP, 5>(a, seed, nblocks, s);
+    case 6: return sig_fo_launch_dpm<DP, 6>(a, seed, nblocks, s);
+    case 7: return sig_fo_launch_dpm<DP, 7>(a, seed, nblocks, s);
+    case 8: return sig_fo_launch_dpm<DP, 8>(a, seed, nblocks, s);
+    default: return GPSIG_EUNSUPPORTED;
+  }
+}
 
 int sig_fo_launch(const SigArgs &a, int DP, int seed, long long nblocks, hipStream_t s) {
   if (fo_geometry(a.l2).W == 0) return GPSIG_EUNSUPPORTED;
   switch (DP) {
 #define CASE(v) \
-  case v: return sig_fo_launch_dp<v>(a, seed, nblocks, s);
+  case v: return fo_dp<v>(a, seed, nblocks, s);
     CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(8) CASE(16) CASE(32)
 #undef CASE
     default: return GPSIG_EUNSUPPORTED;

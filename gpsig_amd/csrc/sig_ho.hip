@@ -88,7 +88,7 @@ __global__ __launch_bounds__(256) void sig_ho_kernel(SigArgs p) {
     RowData<DP> rn;
     rn.load(fx, i + 1 < nrows ? i + 1 : i, SEED);
     float dM[W];
-    seed.row(rd, dM);
+    seed.template row<true>(rd, dM);
 
     float R[ORD][ORD][W];
 #pragma unroll
