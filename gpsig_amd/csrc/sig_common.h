@@ -70,6 +70,9 @@ template <int DP, int W, int SEED>
 struct RowSeed {
   static constexpr int FS = feat_stride(DP);
   static constexpr bool DIFF = (SEED == SEED_RBF_DIFF || SEED == SEED_LIN_DIFF);
+#ifndef GPSIG_D2_RECUR
+#define GPSIG_D2_RECUR 1
+#endif
   static constexpr int ANCHOR = 8;  // exact |x_i - y_j|^2 every ANCHOR rows (d^2 row recurrence between)
   static constexpr float NHL2E = -0.72134752044448170f;  // -log2(e)/2: exp(-d2/2) = exp2(d2 * NHL2E)
   float y[W][DP], dy[W][DP], hdy[W];
@@ -141,9 +144,9 @@ struct RowSeed {
 #pragma unroll
         for (int k = 0; k < DP; ++k) {
           diff[w][k] = rd.x[k] - y[w][k];
-          if constexpr (ANCH) s = __builtin_fmaf(diff[w][k], diff[w][k], s);
+          if constexpr (ANCH || !GPSIG_D2_RECUR) s = __builtin_fmaf(diff[w][k], diff[w][k], s);
         }
-        d2[w] = ANCH ? s : __builtin_fmaf(-2.0f, pp[w], d2[w]);
+        d2[w] = (ANCH || !GPSIG_D2_RECUR) ? s : __builtin_fmaf(-2.0f, pp[w], d2[w]);
         kn[w] = __builtin_amdgcn_exp2f(d2[w] * NHL2E);
       }
       const float knR = lane_next(kn[0]);

@@ -21,7 +21,12 @@ namespace gpsig {
 // DIAGK: the diagonal pass (pairs (a, a)) is the same body under its own symbol, so profiler
 // statistics of the Gram launch are not mixed with it.
 template <int DP, int W, int LP, int M, int SEED, bool DIAGK>
-__global__ __launch_bounds__(256) void sig_fo_kernel(SigArgs p) {
+#ifdef GPSIG_FO_LB
+#define GPSIG_FO_BOUNDS __launch_bounds__(256, GPSIG_FO_LB)
+#else
+#define GPSIG_FO_BOUNDS __launch_bounds__(256)
+#endif
+__global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
   using Seed = RowSeed<DP, W, SEED>;
   constexpr int FS = feat_stride(DP);
   constexpr int G = 64 / LP;
@@ -94,7 +99,10 @@ __global__ __launch_bounds__(256) void sig_fo_kernel(SigArgs p) {
 #pragma unroll
       for (int w = 0; w < W; ++w) C[m + 1][w] = __builtin_fmaf(dM[w], S[m][w], C[m + 1][w]);
   };
-  if constexpr (SEED == SEED_RBF_DIFF && !DIAGK && DP <= 8) {
+#ifndef GPSIG_FO_BLOCKED
+#define GPSIG_FO_BLOCKED 1
+#endif
+  if constexpr (GPSIG_FO_BLOCKED && SEED == SEED_RBF_DIFF && !DIAGK && DP <= 8) {
     // Blocks of ANCHOR rows, fully unrolled (no register rotation at the back edge); the block's
     // last row re-anchors |x - y|^2.  The row records are wave-uniform scalar loads, hoisted.
     constexpr int BLK = Seed::ANCHOR;

@@ -210,7 +210,8 @@ def rescaled(Z: torch.Tensor, X: torch.Tensor, num_levels: int, embedding: str =
     lt, t, d = Z.shape
     n, l, _ = X.shape
     out = torch.empty((num_levels + 1, n, t), dtype=torch.float32, device=X.device)
+    ws = workspace(X.device, lib.gpsig_rescaled_workspace_bytes(n, num_levels))
     rc = lib.gpsig_rescaled(Z.data_ptr(), lt, t, X.data_ptr(), n, l, d, num_levels, EMBEDDINGS[embedding],
-                            out.data_ptr(), _stream(X.device))
+                            out.data_ptr(), ws.data_ptr(), ws.numel(), _stream(X.device))
     L.check(rc, "gpsig_rescaled")
     return out

@@ -113,8 +113,10 @@ int gpsig_tens_vs_seq(const float *Z, int lt, int t, int increments, int d, cons
 int gpsig_tens_gram(const float *Z, int lt, int t, int increments, int d, int num_levels, int base_kind, float *out,
                     gpsig_stream_t stream);
 
+size_t gpsig_rescaled_workspace_bytes(int n, int num_levels);
+
 int gpsig_rescaled(const float *Z, int lt, int t, const float *X, int n, int l, int d, int num_levels,
-                   int embedding, float *out, gpsig_stream_t stream);
+                   int embedding, float *out, void *workspace, size_t workspace_bytes, gpsig_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Goursat PDE (untruncated signature kernel).

@@ -1,0 +1,107 @@
+"""GPU parity of the inducing-tensor kernels (tensor-vs-sequence, tensor Gram, VOSF rescaled) against
+the golden fixtures (tensors.npz / rescaled.npz, pinned to Chen-identity signatures by the oracle)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden, norm_rel_err
+from oracle import kernels_ref as kr
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+
+
+def t(x):
+    return torch.as_tensor(np.asarray(x), device="cuda")
+
+
+def test_tens_vs_seq_linear_order_M_matches_chen():
+    """reference notebooks/signature_kernel.ipynb:225-246 (esig tensor-vs-sequence check)."""
+    from gpsig_amd import ops
+    g = golden("tensors.npz")
+    M = int(g["num_levels"])
+    got = ops.tens_vs_seq(t(g["Z"]), t(g["X"]), M, order=M, base="linear").cpu().numpy()
+    assert (norm_rel_err(got, g["lin_tvs_order5"], axis_levels=True) < TOL).all()
+
+
+@pytest.mark.parametrize("base", ["rbf", "linear"])
+@pytest.mark.parametrize("order", [1, 2, 5])
+@pytest.mark.parametrize("incr", [False, True])
+def test_tens_vs_seq(base, order, incr):
+    from gpsig_amd import ops
+    g = golden("tensors.npz")
+    M = int(g["num_levels"])
+    Z = g["Zi"] if incr else g["Z"] * 0.3
+    got = ops.tens_vs_seq(t(Z), t(g["X"]), M, order=order, base=base, increments=incr).cpu().numpy()
+    exp = g[f"{base}_tvs_incr_o{order}" if incr else f"{base}_tvs_o{order}"]
+    err = norm_rel_err(got, exp, axis_levels=True)
+    assert (err < TOL).all(), err
+
+
+@pytest.mark.parametrize("base", ["rbf", "linear"])
+@pytest.mark.parametrize("incr", [False, True])
+def test_tensor_gram(base, incr):
+    from gpsig_amd import ops
+    g = golden("tensors.npz")
+    M = int(g["num_levels"])
+    Z = g["Zi"] if incr else g["Z"] * 0.3
+    got = ops.tens_gram(t(Z), M, base=base, increments=incr).cpu().numpy()
+    exp = g[f"{base}_tens_incr" if incr else f"{base}_tens"]
+    assert (norm_rel_err(got, exp, axis_levels=True) < TOL).all()
+
+
+def test_tensor_gram_linear_matches_chen():
+    from gpsig_amd import ops
+    g = golden("tensors.npz")
+    got = ops.tens_gram(t(g["Z"]), int(g["num_levels"]), base="linear").cpu().numpy()
+    assert (norm_rel_err(got, g["lin_tens"], axis_levels=True) < TOL).all()
+
+
+def test_K_tens_vs_seq_normalised_kernel_api():
+    import gpsig_amd
+    g = golden("tensors.npz")
+    X, M = g["X"], int(g["num_levels"])
+    N, L, D = X.shape
+    k = gpsig_amd.SignatureRBF(L * D, D, M)
+    got = k.K_tens_vs_seq(t(g["Z"] * 0.3), t(X.reshape(N, -1)), return_levels=True).cpu().numpy()
+    assert (norm_rel_err(got, g["rbf_Kuf_norm_levels"], axis_levels=True) < TOL).all()
+
+
+@pytest.mark.parametrize("full_X_cov", [False, True])
+def test_K_tens_n_seq_covs_vs_oracle(full_X_cov):
+    import gpsig_amd
+    g = golden("tensors.npz")
+    X, M = g["X"], int(g["num_levels"])
+    N, L, D = X.shape
+    Z = g["Z"] * 0.3
+    k = gpsig_amd.SignatureRBF(L * D, D, M)
+    ref = kr.SignatureKernelRef(L * D, D, M)
+    got = k.K_tens_n_seq_covs(t(Z), t(X.reshape(N, -1)), full_X_cov=full_X_cov, return_levels=True)
+    exp = ref.K_tens_n_seq_covs(Z, X.reshape(N, -1), full_X_cov=full_X_cov, return_levels=True)
+    for a, b in zip(got, exp):
+        assert (norm_rel_err(a.cpu().numpy(), b, axis_levels=True) < TOL).all()
+
+
+@pytest.mark.parametrize("emb", ["linear", "rbf"])
+def test_rescaled_vosf(emb):
+    from gpsig_amd import ops
+    g = golden("rescaled.npz")
+    M = int(g["num_levels"])
+    got = ops.rescaled(t(g["Z"]), t(g["X"]), M, embedding=emb).cpu().numpy()
+    exp = g["K_linear" if emb == "linear" else "K_rbf"]
+    err = norm_rel_err(got[1:], exp[1:], axis_levels=True)
+    assert (err < TOL).all(), err
+    np.testing.assert_allclose(got[0], 0.0)
+
+
+def test_mahalanobis_kernel_api():
+    import gpsig_amd
+    g = golden("rescaled.npz")
+    X, Z, M = g["X"], g["Z"], int(g["num_levels"])
+    N, L, D = X.shape
+    Zfull = np.concatenate([np.full((1, Z.shape[1], D), 0.7), Z], axis=0)
+    k = gpsig_amd.SignatureLinear(L * D, D, M, normalization=False)
+    ref = kr.SignatureKernelRef(L * D, D, M, base="linear", normalization=False)
+    got = k.Mahalanobis_term_approx_posterior(t(Zfull), t(X.reshape(N, -1))).cpu().numpy()
+    exp = ref.Mahalanobis_term_approx_posterior(Zfull, X.reshape(N, -1))
+    assert norm_rel_err(got, exp) < TOL
