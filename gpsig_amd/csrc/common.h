@@ -41,6 +41,36 @@ GPSIG_DEV float group_incl_scan(float v) {
   return v;
 }
 
+// N independent inclusive group scans, step-interleaved so consecutive DPP reads never wait on the
+// VALU result of the previous step (the VALU-write -> DPP-read hazard otherwise costs s_nops).
+template <int LP, int N>
+GPSIG_DEV void group_incl_scan_n(float (&v)[N]) {
+  static_assert(LP == 16 || LP == 32 || LP == 64, "LP");
+#pragma unroll
+  for (int k = 0; k < N; ++k) v[k] += dpp_f<0x111>(v[k]);
+#pragma unroll
+  for (int k = 0; k < N; ++k) v[k] += dpp_f<0x112>(v[k]);
+#pragma unroll
+  for (int k = 0; k < N; ++k) v[k] += dpp_f<0x114>(v[k]);
+#pragma unroll
+  for (int k = 0; k < N; ++k) v[k] += dpp_f<0x118>(v[k]);
+  // The row broadcasts run over all rows and their term is weighted by a per-lane 0/1 factor
+  // instead of a row-masked DPP (which needs a freshly zeroed destination per step): row_bcast:15
+  // feeds rows 1 and 3 only (row 2 belongs to the next group at LP = 32 and takes rows 0-1 through
+  // row_bcast:31 at LP = 64).
+  const int row = (int)(__lane_id() >> 4);
+  if constexpr (LP >= 32) {
+    const float f = (row & 1) ? 1.0f : 0.0f;
+#pragma unroll
+    for (int k = 0; k < N; ++k) v[k] = __builtin_fmaf(dpp_f<0x142>(v[k]), f, v[k]);
+  }
+  if constexpr (LP >= 64) {
+    const float f = (row >= 2) ? 1.0f : 0.0f;
+#pragma unroll
+    for (int k = 0; k < N; ++k) v[k] = __builtin_fmaf(dpp_f<0x143>(v[k]), f, v[k]);
+  }
+}
+
 // Value of lane (lane+1) of the wave (0 for lane 63).
 GPSIG_DEV float lane_next(float v) { return dpp_f<0x130>(v); }
 // Value of lane (lane-1) of the wave (`edge` for lane 0 is handled by the caller).
@@ -70,6 +100,38 @@ GPSIG_DEV float em1_small(float x) {
   p = __builtin_fmaf(p, x, 4.999998314e-01f);
   p = __builtin_fmaf(p, x, 1.000000095e+00f);
   return p * x;
+}
+
+// Packed fp32 pairs: on gfx950 v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32 process two fp32 values
+// per lane in one VALU issue (a wave-uniform SGPR operand is broadcast through op_sel), so every
+// per-cell evaluation is written on column pairs.
+typedef float f2 __attribute__((ext_vector_type(2)));
+GPSIG_DEV f2 splat2(float v) { return (f2){v, v}; }
+GPSIG_DEV f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
+GPSIG_DEV f2 em1_small2(f2 x) {
+  f2 p = splat2(1.388882549e-03f);
+  p = fma2(p, x, splat2(8.407682727e-03f));
+  p = fma2(p, x, splat2(4.166870013e-02f));
+  p = fma2(p, x, splat2(1.666597426e-01f));
+  p = fma2(p, x, splat2(4.999998314e-01f));
+  p = fma2(p, x, splat2(1.000000095e+00f));
+  return p * x;
+}
+
+// N independent em1 evaluations, Horner steps interleaved across the N chains (back-to-back
+// dependent v_pk_fma_f32 would otherwise be padded with s_nop).
+template <int N>
+GPSIG_DEV void em1_small2_n(const f2 (&x)[N], f2 (&out)[N]) {
+  constexpr float c[6] = {1.388882549e-03f, 8.407682727e-03f, 4.166870013e-02f,
+                          1.666597426e-01f, 4.999998314e-01f, 1.000000095e+00f};
+#pragma unroll
+  for (int k = 0; k < N; ++k) out[k] = fma2(splat2(c[0]), x[k], splat2(c[1]));
+#pragma unroll
+  for (int s = 2; s < 6; ++s)
+#pragma unroll
+    for (int k = 0; k < N; ++k) out[k] = fma2(out[k], x[k], splat2(c[s]));
+#pragma unroll
+  for (int k = 0; k < N; ++k) out[k] = out[k] * x[k];
 }
 
 // exp(x) = 2^(x log2 e) on the hardware transcendental unit (v_exp_f32, ~1 ulp).

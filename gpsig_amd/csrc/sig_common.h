@@ -6,8 +6,9 @@
 
 namespace gpsig {
 
-// Per-point feature record, FS floats (16-byte aligned): [x (DP) | dx (DP) | |dx|^2/2 | pad...]
-// dx_i = x_{i+1} - x_i (zero for the last point).  DP = padded channel count of the instantiation.
+// Per-point feature record, FS floats (16-byte aligned): [x (DP) | dx (DP) | |dx|^2/2 | g | pad...]
+// dx_i = x_{i+1} - x_i (zero for the last point), g_i = <x_i, dx_i> + |dx_i|^2/2 (2*DP+1 is odd, so
+// the record always has this slot).  DP = padded channel count of the instantiation.
 __host__ __device__ constexpr int feat_stride(int DP) { return ((2 * DP + 1) + 3) & ~3; }
 
 enum Seed : int {
@@ -38,7 +39,7 @@ struct SigArgs {
 // Wave-uniform record of row i: x_{i+1} (RBF DIFF) or x_i (POINT seeds), dx_i, |dx_i|^2/2.
 template <int DP>
 struct RowData {
-  float x[DP], dx[DP], hdx;
+  float x[DP], dx[DP], hdx, g;
   GPSIG_DEV void load(const float *__restrict__ fx, int i, int seed) {
     constexpr int FS = feat_stride(DP);
     const float *__restrict__ fr = fx + (long long)i * FS;
@@ -49,6 +50,7 @@ struct RowData {
       dx[k] = fr[DP + k];
     }
     hdx = fr[2 * DP];
+    g = fr[2 * DP + 1];
   }
 };
 
@@ -196,6 +198,190 @@ struct RowSeed {
     }
   }
 };
+
+// ---------------------------------------------------------------------------------------------
+// RBF DIFF seed on column pairs (first-order kernel; W even).  Same cells as RowSeed<.., RBF_DIFF>,
+// with the per-row work cut to what the recursion needs and laid out for v_pk_* instructions.
+// With p_ij = <y_j, dx_i> - g_i (g_i from the feature record), c_ij = <dx_i, dy_j> and
+// q_ij = <x_i - y_j, dy_j> - |dy_j|^2/2, the cell is k(x_i,y_j) (Ep Eq + (1 + Ep)(1 + Eq) Ec),
+// E* = expm1(*), and both row-to-row quantities follow from what the cell already computed:
+//   k(x_{i+1}, y_j) = k(x_i, y_j) (1 + Ep_ij)          q_{i+1,j} = q_ij + c_ij
+//   Eq_{i+1,j} = Eq_ij + Ec_ij + Eq_ij Ec_ij           (= expm1(q_ij + c_ij), no cancellation)
+// so a row costs two packed dots, two polynomial expm1 (p, c) and a few FMAs per column pair: no
+// exp.  k and Eq are re-evaluated exactly from x_{i+1} - y_j on anchor rows (every ANCHOR rows), so
+// rounding drift is bounded by ANCHOR steps.  When |p| or |c| of some cell of the wave reaches
+// EM1_TAU (a wave-uniform branch), the next row is evaluated exactly and those cells take the plain
+// corner difference of the k grid.
+#ifndef GPSIG_NAIVE
+#define GPSIG_NAIVE 1
+#endif
+template <int DP, int W>
+struct RbfSeedPk {
+  static_assert(W % 2 == 0, "column pairs");
+  static constexpr int W2 = W / 2;
+  static constexpr int FS = feat_stride(DP);
+#ifndef GPSIG_PK_ANCHOR
+#define GPSIG_PK_ANCHOR 8
+#endif
+  static constexpr int ANCHOR = GPSIG_PK_ANCHOR;
+  static constexpr float NHL2E = -0.72134752044448170f;  // exp(-d2/2) = exp2(d2 * NHL2E)
+  static constexpr float L2E = 1.4426950408889634f;
+  f2 y[W2][DP], dy[W2][DP], hdy[W2];
+  f2 Eq[W2], kc[W2];  // expm1(q_ij), k(x_i, y_j)
+  float kcR;          // next lane's kc of its first column
+  bool valid_last;
+
+  GPSIG_DEV void init(const float *__restrict__ fx, const float *__restrict__ fy, int gl, int l2) {
+    const int ncols = l2 - 1;
+    // columns past the sequence clamp to its last point (zero increment): their cells are exact
+    // zeros in the product form; only the lane's last column can see a foreign right neighbour
+#pragma unroll
+    for (int w2 = 0; w2 < W2; ++w2)
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int j = gl * W + 2 * w2 + h;
+        const int jj = j < l2 ? j : l2 - 1;
+        const float *f = fy + (long long)jj * FS;
+#pragma unroll
+        for (int k = 0; k < DP; ++k) {
+          y[w2][k][h] = f[k];
+          dy[w2][k][h] = f[DP + k];
+        }
+        hdy[w2][h] = f[2 * DP];
+        if (w2 == W2 - 1 && h == 1) valid_last = j < ncols;
+      }
+    float x0[DP];
+#pragma unroll
+    for (int k = 0; k < DP; ++k) x0[k] = fx[k];
+    exact(x0, Eq, kc);
+    kcR = lane_next(kc[0][0]);
+  }
+
+  // expm1(q) and k(x, y) of the row with point x, evaluated from x - y
+  GPSIG_DEV void exact(const float (&x)[DP], f2 (&Eqo)[W2], f2 (&ko)[W2]) const {
+#pragma unroll
+    for (int w2 = 0; w2 < W2; ++w2) {
+      f2 s = splat2(0.0f), qq = -hdy[w2];
+#pragma unroll
+      for (int k = 0; k < DP; ++k) {
+        const f2 df = splat2(x[k]) - y[w2][k];
+        s = fma2(df, df, s);
+        qq = fma2(df, dy[w2][k], qq);
+      }
+      s = s * splat2(NHL2E);
+      Eqo[w2] = em1_small2(qq);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        ko[w2][h] = __builtin_amdgcn_exp2f(s[h]);
+        // outside the polynomial range expm1(q) = e^q - 1 loses nothing that matters
+        if (!(__builtin_fabsf(qq[h]) < EM1_TAU)) Eqo[w2][h] = __builtin_amdgcn_exp2f(qq[h] * L2E) - 1.0f;
+      }
+    }
+  }
+
+  // Wave-uniform part of row i's record the recurrences need (x_{i+1} is read only on anchor rows
+  // and slow rows, straight from the record).
+  struct Row {
+    float dx[DP], g;
+    const float *fr;  // record of row i; x_{i+1} = fr[FS .. FS + DP)
+    GPSIG_DEV void load(const float *__restrict__ fx, int i) {
+      fr = fx + (long long)i * FS;
+#pragma unroll
+      for (int k = 0; k < DP; ++k) dx[k] = fr[DP + k];
+      g = fr[2 * DP + 1];
+    }
+  };
+
+  GPSIG_DEV void next_exact(const Row &rd, f2 (&Eqo)[W2], f2 (&ko)[W2]) const {
+    float x1[DP];
+#pragma unroll
+    for (int k = 0; k < DP; ++k) x1[k] = rd.fr[FS + k];
+    exact(x1, Eqo, ko);
+  }
+
+  // Cells of row i into dM.  anch (wave-uniform): the next row's state is re-evaluated exactly
+  // instead of by the recurrences.
+  GPSIG_DEV void row(const Row &rd, bool anch, f2 (&dM)[W2]) {
+    f2 p[W2], c[W2], Eqn[W2], kn[W2];
+#pragma unroll
+    for (int w2 = 0; w2 < W2; ++w2) {
+      f2 a = splat2(-rd.g), cc = splat2(0.0f);
+#pragma unroll
+      for (int k = 0; k < DP; ++k) {
+        a = fma2(y[w2][k], splat2(rd.dx[k]), a);
+        cc = fma2(dy[w2][k], splat2(rd.dx[k]), cc);
+      }
+      p[w2] = a;
+      c[w2] = cc;
+    }
+    f2 Ep[W2], Ec[W2];
+    em1_small2_n<W2>(p, Ep);
+    em1_small2_n<W2>(c, Ec);
+    float mx = 0.0f;
+#pragma unroll
+    for (int w2 = 0; w2 < W2; ++w2) {
+      f2 t = fma2(Ep[w2], Ec[w2], Ec[w2]);
+      t = fma2(Eq[w2], t, t);
+      dM[w2] = kc[w2] * fma2(Ep[w2], Eq[w2], t);
+      kn[w2] = fma2(kc[w2], Ep[w2], kc[w2]);
+      Eqn[w2] = fma2(Eq[w2], Ec[w2], Eq[w2] + Ec[w2]);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) mx = __builtin_fmaxf(__builtin_fmaxf(mx, __builtin_fabsf(p[w2][h])), __builtin_fabsf(c[w2][h]));
+    }
+    const bool slow = GPSIG_NAIVE && __builtin_amdgcn_ballot_w64(mx >= EM1_TAU) != 0;
+    if (anch || slow) next_exact(rd, Eqn, kn);
+    const float knR = lane_next(kn[0][0]);
+    if (slow) {
+      // corner difference k11 - k10 - k01 + k00 for the cells outside the polynomial range
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        const int w2 = w / 2, h = w % 2;
+        const float kn1 = (w + 1 < W) ? kn[(w + 1) / 2][(w + 1) % 2] : knR;
+        const float kc1 = (w + 1 < W) ? kc[(w + 1) / 2][(w + 1) % 2] : kcR;
+        const float naive = (kn1 - kn[w2][h]) - (kc1 - kc[w2][h]);
+        const float m = __builtin_fmaxf(__builtin_fabsf(p[w2][h]), __builtin_fabsf(c[w2][h]));
+        float v = m < EM1_TAU ? dM[w2][h] : naive;
+        if (w + 1 == W && !valid_last) v = 0.0f;
+        dM[w2][h] = v;
+      }
+    }
+#pragma unroll
+    for (int w2 = 0; w2 < W2; ++w2) {
+      Eq[w2] = Eqn[w2];
+      kc[w2] = kn[w2];
+    }
+    kcR = knR;
+  }
+};
+
+// ---------------------------------------------------------------------------------------------
+// Level 1 of a DIFF seed in closed form.  K_1 = sum_ij dM_ij telescopes to the corner difference
+// k(x_L, y_L) - k(x_L, y_0) - k(x_0, y_L) + k(x_0, y_0) (linear: <x_L - x_0, y_L - y_0>), evaluated
+// once per pair in fp64.  The fp32 row sums of dM cancel down to K_1 and lose ~1e-7 of sum|dM|,
+// which is the whole error budget when K_1 is small against the cells (K_1 feeds only level 1).
+template <int DP, int SEED>
+GPSIG_DEV float level1_closed(const float *__restrict__ fx, const float *__restrict__ fy, int l1, int l2) {
+  constexpr int FS = feat_stride(DP);
+  const float *x0 = fx, *xl = fx + (long long)(l1 - 1) * FS;
+  const float *y0 = fy, *yl = fy + (long long)(l2 - 1) * FS;
+  if constexpr (SEED == SEED_RBF_DIFF) {
+    auto k = [](const float *a, const float *b) {
+      double s = 0.0;
+#pragma unroll
+      for (int c = 0; c < DP; ++c) {
+        const double d = (double)a[c] - (double)b[c];
+        s = __builtin_fma(d, d, s);
+      }
+      return exp(-0.5 * s);
+    };
+    return (float)((k(xl, yl) - k(xl, y0)) - (k(x0, yl) - k(x0, y0)));
+  } else {
+    double s = 0.0;
+#pragma unroll
+    for (int c = 0; c < DP; ++c) s = __builtin_fma((double)xl[c] - (double)x0[c], (double)yl[c] - (double)y0[c], s);
+    return (float)s;
+  }
+}
 
 // ---------------------------------------------------------------------------------------------
 // Tile scheduler.  A workgroup = 4 waves; wave w takes sequence a = 4*ta + w; the wave's G = 64/LP

@@ -64,73 +64,86 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
   const float *__restrict__ fx = p.FX + (long long)a * p.l1 * FS;
   const float *__restrict__ fy = p.FY + (long long)bl * p.l2 * FS;
 
-  Seed seed;
+  constexpr bool PK = (SEED == SEED_RBF_DIFF);
+  using PSeed = std::conditional_t<PK, RbfSeedPk<DP, W>, RowSeed<DP, W, SEED>>;
+  constexpr int W2 = W / 2;
+  PSeed seed;
   seed.init(fx, fy, gl, p.l2);
 
-  float C[M][W];
+  f2 C[M][W2];
 #pragma unroll
   for (int m = 0; m < M; ++m)
 #pragma unroll
-    for (int w = 0; w < W; ++w) C[m][w] = 0.0f;
+    for (int w2 = 0; w2 < W2; ++w2) C[m][w2] = splat2(0.0f);
 
   const int nrows = Seed::DIFF ? p.l1 - 1 : p.l1;
   // One row: seed cells, then the level recursion.  S_m = exclusive prefix over (rows < i, cols < j)
   // of R_m = exclusive scan over j of C_m; the M-1 scans are independent and interleave.
-  auto do_row = [&](const RowData<DP> &rd, auto anch) {
-    float dM[W];
-    seed.template row<decltype(anch)::value>(rd, dM);
-    float S[M > 1 ? M - 1 : 1][W];
+  using Rec = std::conditional_t<PK, typename RbfSeedPk<DP, W>::Row, RowData<DP>>;
+  auto do_row = [&](const Rec &rd, bool anch) {
+    f2 dM[W2];
+    if constexpr (PK) {
+      seed.row(rd, anch, dM);
+    } else {
+      float d1[W];
+      seed.template row<true>(rd, d1);
+#pragma unroll
+      for (int w2 = 0; w2 < W2; ++w2) dM[w2] = (f2){d1[2 * w2], d1[2 * w2 + 1]};
+    }
+    // lane totals of C_m (pair tree), scanned across the group for all M-1 levels together; then
+    // S_m(j) = (exclusive cross-lane prefix) + (exclusive in-lane prefix), written straight into
+    // the column pairs
+    constexpr int ML = M > 1 ? M - 1 : 1;
+    float T[ML], base[ML];
 #pragma unroll
     for (int m = 0; m + 1 < M; ++m) {
-      float t[W];
-      t[0] = C[m][0];
+      f2 s2 = C[m][0];
 #pragma unroll
-      for (int w = 1; w < W; ++w) t[w] = t[w - 1] + C[m][w];
-      const float incl = group_incl_scan<LP>(t[W - 1]);
-      const float base = incl - t[W - 1];
-      S[m][0] = base;
+      for (int w2 = 1; w2 < W2; ++w2) s2 += C[m][w2];
+      T[m] = s2[0] + s2[1];
+      base[m] = T[m];
+    }
+    if constexpr (M > 1) group_incl_scan_n<LP, ML>(base);
+    // descending m: level m reads C_m before level m-1's update writes it
 #pragma unroll
-      for (int w = 1; w < W; ++w) S[m][w] = base + t[w - 1];
+    for (int m = M - 2; m >= 0; --m) {
+      f2 S[W2];
+      S[0][0] = base[m] - T[m];
+#pragma unroll
+      for (int w = 1; w < W; ++w) S[w / 2][w % 2] = S[(w - 1) / 2][(w - 1) % 2] + C[m][(w - 1) / 2][(w - 1) % 2];
+#pragma unroll
+      for (int w2 = 0; w2 < W2; ++w2) C[m + 1][w2] = fma2(dM[w2], S[w2], C[m + 1][w2]);
     }
 #pragma unroll
-    for (int w = 0; w < W; ++w) C[0][w] += dM[w];
-#pragma unroll
-    for (int m = 0; m + 1 < M; ++m)
-#pragma unroll
-      for (int w = 0; w < W; ++w) C[m + 1][w] = __builtin_fmaf(dM[w], S[m][w], C[m + 1][w]);
+    for (int w2 = 0; w2 < W2; ++w2) C[0][w2] += dM[w2];
   };
-#ifndef GPSIG_FO_BLOCKED
-#define GPSIG_FO_BLOCKED 1
+  // Row loop.  For the packed RBF seed the row recurrences are re-anchored every ANCHOR rows (a
+  // wave-uniform branch); the other seeds evaluate every row directly.
+#ifndef GPSIG_FO_UNROLL2
+#define GPSIG_FO_UNROLL2 (W <= 4)
 #endif
-  if constexpr (GPSIG_FO_BLOCKED && SEED == SEED_RBF_DIFF && !DIAGK && DP <= 8) {
-    // Blocks of ANCHOR rows, fully unrolled (no register rotation at the back edge); the block's
-    // last row re-anchors |x - y|^2.  The row records are wave-uniform scalar loads, hoisted.
-    constexpr int BLK = Seed::ANCHOR;
-    int i = 0;
-    for (; i + BLK <= nrows; i += BLK) {
-      RowData<DP> rd[BLK];
-#pragma unroll
-      for (int u = 0; u < BLK; ++u) rd[u].load(fx, i + u, SEED);
-#pragma unroll
-      for (int u = 0; u < BLK; ++u) {
-        if (u + 1 < BLK)
-          do_row(rd[u], std::false_type{});
-        else
-          do_row(rd[u], std::true_type{});
-      }
+  int i = 0;
+  if constexpr (PK && GPSIG_FO_UNROLL2) {
+    // row pairs: ANCHOR is even, so the first row of a pair never anchors (compile-time)
+    static_assert(PSeed::ANCHOR % 2 == 0, "anchor period");
+    for (; i + 2 <= nrows; i += 2) {
+      Rec r0, r1;
+      r0.load(fx, i);
+      r1.load(fx, i + 1);
+      do_row(r0, false);
+      do_row(r1, ((i + 1) % PSeed::ANCHOR) == PSeed::ANCHOR - 1);
     }
-    for (; i < nrows; ++i) {
-      RowData<DP> rd;
+  }
+  for (; i < nrows; ++i) {
+    Rec rd;
+    bool anch = true;
+    if constexpr (PK) {
+      rd.load(fx, i);
+      anch = (i % PSeed::ANCHOR) == PSeed::ANCHOR - 1;
+    } else {
       rd.load(fx, i, SEED);
-      do_row(rd, std::true_type{});
     }
-  } else {
-    // plain row loop (diagonal pass, cheap seeds); RBF distances evaluated exactly every row
-    for (int i = 0; i < nrows; ++i) {
-      RowData<DP> rd;
-      rd.load(fx, i, SEED);
-      do_row(rd, std::true_type{});
-    }
+    do_row(rd, anch);
   }
 
   // ---- epilogue: K_m = sum_j C_m(j)
@@ -138,20 +151,23 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
   K[0] = 1.0f;
 #pragma unroll
   for (int m = 0; m < M; ++m) {
-    float s = 0.0f;
+    f2 s2 = C[m][0];
 #pragma unroll
-    for (int w = 0; w < W; ++w) s += C[m][w];
-    K[m + 1] = group_sum<LP>(s);
+    for (int w2 = 1; w2 < W2; ++w2) s2 += C[m][w2];
+    K[m + 1] = group_sum<LP>(s2[0] + s2[1]);
   }
-  if (gl == 0 && pair_ok) store_pair<M>(p, a, b, K);
+  if (gl == 0 && pair_ok) {
+    if constexpr (Seed::DIFF) K[1] = level1_closed<DP, SEED>(fx, fy, p.l1, p.l2);
+    store_pair<M>(p, a, b, K);
+  }
 }
 
 // Column geometry: W columns per lane, LP lanes per pair; capacity LP*W >= points per sequence.
 struct Geo { int W, LP; };
 inline Geo fo_geometry(int l2) {
   if (l2 <= 64) return {4, 16};
-  if (l2 <= 128) return {4, 32};
-  if (l2 <= 256) return {4, 64};
+  if (l2 <= 128) return {8, 16};
+  if (l2 <= 256) return {8, 32};
   if (l2 <= 512) return {8, 64};
   return {0, 0};
 }
@@ -171,8 +187,8 @@ template <int DP, int M, int SEED>
 int fo_geo(const SigArgs &a, long long nblocks, hipStream_t s) {
   const Geo geo = fo_geometry(a.l2);
   if (geo.W == 4 && geo.LP == 16) return launch_fo<DP, 4, 16, M, SEED>(a, nblocks, s);
-  if (geo.W == 4 && geo.LP == 32) return launch_fo<DP, 4, 32, M, SEED>(a, nblocks, s);
-  if (geo.W == 4 && geo.LP == 64) return launch_fo<DP, 4, 64, M, SEED>(a, nblocks, s);
+  if (geo.W == 8 && geo.LP == 16) return launch_fo<DP, 8, 16, M, SEED>(a, nblocks, s);
+  if (geo.W == 8 && geo.LP == 32) return launch_fo<DP, 8, 32, M, SEED>(a, nblocks, s);
   if (geo.W == 8 && geo.LP == 64) return launch_fo<DP, 8, 64, M, SEED>(a, nblocks, s);
   return GPSIG_EUNSUPPORTED;
 }

@@ -25,6 +25,7 @@ __global__ __launch_bounds__(256) void features_kernel(const float *__restrict__
   constexpr int FS = feat_stride(DP);
   float *f = F + idx * FS;
   float h = 0.0f;
+  double gx = 0.0;  // <x, dx> accumulated in fp64, rounded once
 #pragma unroll
   for (int k = 0; k < DP; ++k) {
     const float xv = k < d ? x[k] : 0.0f;
@@ -32,10 +33,12 @@ __global__ __launch_bounds__(256) void features_kernel(const float *__restrict__
     f[k] = xv;
     f[DP + k] = dv;
     h = __builtin_fmaf(dv, dv, h);
+    gx = __builtin_fma((double)xv, (double)dv, gx);
   }
   f[2 * DP] = 0.5f * h;
+  f[2 * DP + 1] = (float)(gx + 0.5 * (double)h);
 #pragma unroll
-  for (int k = 2 * DP + 1; k < FS; ++k) f[k] = 0.0f;
+  for (int k = 2 * DP + 2; k < FS; ++k) f[k] = 0.0f;
 }
 
 // ------------------------------------------------------------------------------------ launchers

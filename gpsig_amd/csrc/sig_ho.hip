@@ -183,7 +183,10 @@ __global__ __launch_bounds__(256) void sig_ho_kernel(SigArgs p) {
       for (int w = 0; w < W; ++w) s += CB[Lay::off(m) + x][w];
     K[m] = group_sum<64>(s);
   }
-  if (lane == 0) store_pair<MMAX>(p, a, b, K);
+  if (lane == 0) {
+    K[1] = level1_closed<DP, SEED>(fx, fy, p.l1, p.l2);  // ho seeds are the DIFF seeds
+    store_pair<MMAX>(p, a, b, K);
+  }
 }
 
 template <int DP, int W, int ORD, int SEED>

@@ -20,6 +20,12 @@
 #ifndef KL
 #define KL 128
 #endif
+#ifndef KW
+#define KW 4
+#endif
+#ifndef KLP
+#define KLP 32
+#endif
 
 using namespace gpsig;
 
@@ -62,6 +68,9 @@ int main(int argc, char **argv) {
         h += dv * dv;
       }
       F[((size_t)a * l + i) * FS + 2 * DP] = 0.5f * h;
+      double gx = 0;
+      for (int k = 0; k < DP; ++k) gx += (double)F[((size_t)a * l + i) * FS + k] * F[((size_t)a * l + i) * FS + DP + k];
+      F[((size_t)a * l + i) * FS + 2 * DP + 1] = (float)(gx + 0.5 * h);
     }
   float *dF, *dOut;
   CK(hipMalloc(&dF, F.size() * 4));
@@ -83,7 +92,7 @@ int main(int argc, char **argv) {
   p.out_rows = n;
   p.out_ld = n;
   p.out_lvl = (long long)n * n;
-  const Geo geo = fo_geometry(l);
+  const Geo geo{KW, KLP};
   const int G = 64 / geo.LP, k = 4 / G;
   const long long ntb = (n + G - 1) / G, nta = (n + 3) / 4;
   p.ntb = (int)ntb;
@@ -93,7 +102,7 @@ int main(int argc, char **argv) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   auto launch = [&]() {
-    hipLaunchKernelGGL((sig_fo_kernel<DP, 4, (KL <= 64 ? 16 : KL <= 128 ? 32 : 64), KM, SEED_RBF_DIFF, false>),
+    hipLaunchKernelGGL((sig_fo_kernel<DP, KW, KLP, KM, SEED_RBF_DIFF, false>),
                        dim3((unsigned)nblocks), dim3(256), 0, 0, p);
   };
   launch();
