@@ -89,7 +89,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-check", action="store_true")
-    ap.add_argument("--traffic-json", default=None,
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r1_gram_counters.json"),
                     help="per-launch HBM bytes of the Gram kernel from a PMC pass (profiles/*.json)")
     args = ap.parse_args()
 
@@ -164,10 +164,12 @@ def main():
     b_entry = 4 * (l - 1) * (l - 1) + 4 * (m + 1)
     avg_launch_s = kern_ms / 1e3 / max(launches, 1)
     achieved = entries_per_launch * b_entry / avg_launch_s / 1e9
-    traffic = None
-    if args.traffic_json and os.path.exists(args.traffic_json):
+    traffic, prof = None, {}
+    # the committed profile is of the default workload; other workloads report traffic null
+    if args.traffic_json and os.path.exists(args.traffic_json) and args.workload == "H" and not args.n:
         with open(args.traffic_json) as f:
-            traffic = json.load(f).get("hbm_bytes_per_launch")
+            prof = json.load(f)
+        traffic = prof.get("hbm_bytes_per_launch")
 
     value = args.steps * n * n / elapsed
     out = {
@@ -188,7 +190,10 @@ def main():
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "sig_fo_kernel", "launch_ms": avg_launch_s * 1e3, "bytes_per_entry": b_entry,
-                     "entries_per_launch": entries_per_launch},
+                     "entries_per_launch": entries_per_launch,
+                     # the fused kernel never materialises the tile: physically it is VALU-issue bound
+                     "physical_bound": "valu", "valu_issue_util": prof.get("valu_issue_util"),
+                     "profile": args.traffic_json if prof else None},
     }
     if rank == 0 and not args.no_check:
         # parity on a bounded subsample: the normalised Gram restricted to a subset S of the sequences
