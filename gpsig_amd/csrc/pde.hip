@@ -148,6 +148,173 @@ __global__ __launch_bounds__(256) void pde_kernel(PdeArgs p) {
   }
 }
 
+// Coarse-row stepping (REP = 2^dyadic fine rows per step).  The increment of a coarse cell is shared
+// by its REP x REP fine cells (sigKer_fast.pyx:35-43 recomputes it per fine cell), so each step
+// evaluates the lane's W/REP coarse increments and update coefficients once and then sweeps REP fine
+// rows x W fine columns; the skew is one step per coarse row, the left boundary of the REP rows comes
+// from lane l-1 (REP DPP moves per step).
+template <typename T, int DP, int W, int REP>
+__global__ __launch_bounds__(256) void pde_rep_kernel(PdeArgs p) {
+  static_assert(W % REP == 0, "a lane owns whole coarse columns");
+  constexpr int WC = W / REP;
+  extern __shared__ __attribute__((aligned(16))) float lds[];
+  const int lane = threadIdx.x & 63;
+  const int wave = wave_uniform(threadIdx.x >> 6);
+
+  int a, b;
+  if (p.pair_mode == GPSIG_PAIRS_DIAG) {
+    a = p.row_begin + (int)blockIdx.x * 4 + wave;
+    b = a;
+  } else {
+    int ta, tb;
+    if (p.pair_mode == GPSIG_PAIRS_UPPER) {
+      const Tile t = upper_tile(p.tile_base + (long long)blockIdx.x, p.ntb, 4);
+      ta = t.ta;
+      tb = t.tb;
+    } else {
+      ta = p.tiles_a0 + (int)blockIdx.x / p.ntb;
+      tb = (int)blockIdx.x % p.ntb;
+    }
+    a = ta * 4 + wave;
+    b = tb;
+  }
+  // wave-uniform validity; every wave still reaches the LDS barrier below
+  bool ok = a >= p.row_begin && a < p.row_end && b < p.n2;
+  if (p.pair_mode == GPSIG_PAIRS_UPPER && b < a) ok = false;
+  if (!ok) { a = p.row_begin; b = p.pair_mode == GPSIG_PAIRS_RECT ? 0 : a; }
+
+  const T inv_factor = (T)1.0 / (T)(REP * REP);
+  const int IC = p.l1 - 1, JC = p.l2 - 1;  // coarse rows / columns
+  const int J = REP * JC;
+  const int d = p.d;
+  const float *x = p.X + (long long)a * p.l1 * d;
+  const float *y = p.Y + (long long)b * p.l2 * d;
+
+  float *dxs = lds + (size_t)wave * IC * DP;
+  for (int r = lane; r < IC; r += 64)
+#pragma unroll
+    for (int k = 0; k < DP; ++k) dxs[r * DP + k] = k < d ? x[(r + 1) * d + k] - x[r * d + k] : 0.0f;
+
+  // y increments of this lane's coarse columns
+  float dy[WC][DP];
+#pragma unroll
+  for (int w = 0; w < WC; ++w) {
+    int cj = lane * WC + w;
+    cj = cj < JC - 1 ? cj : JC - 1;
+#pragma unroll
+    for (int k = 0; k < DP; ++k) dy[w][k] = k < d ? y[(cj + 1) * d + k] - y[cj * d + k] : 0.0f;
+  }
+  __syncthreads();
+  if (!ok) return;
+
+  const bool hybrid = (p.pair_mode == GPSIG_PAIRS_DIAG) && p.solver == 0;
+  const bool s1 = p.solver == 1;
+  T up[W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) up[w] = (T)1;
+  T last[REP];  // K[row][lane*W + W - 1] of this lane's REP rows of the previous step
+#pragma unroll
+  for (int r = 0; r < REP; ++r) last[r] = (T)1;
+  T corner_prev = (T)1;  // left boundary of the previous step's last row
+  const int lanes_used = (J + W - 1) / W;
+  const int nsteps = IC + lanes_used - 1;
+  for (int s = 0; s < nsteps; ++s) {
+    T left[REP];
+#pragma unroll
+    for (int r = 0; r < REP; ++r) {
+      left[r] = lane_prev(last[r]);
+      if (lane == 0) left[r] = (T)1;
+    }
+    const int ci = s - lane;
+    if (ci >= 0 && ci < IC && lane < lanes_used) {
+      const float *dxr = dxs + ci * DP;
+      float dxv[DP];
+#pragma unroll
+      for (int k = 0; k < DP; ++k) dxv[k] = dxr[k];
+      // coefficients of the lane's coarse cells: solver 1 uses (A, B), solver 0 uses inc - 1 (as B)
+      T A[WC], B[WC];
+#pragma unroll
+      for (int w = 0; w < WC; ++w) {
+        float incf = 0.0f;
+#pragma unroll
+        for (int k = 0; k < DP; ++k) incf = __builtin_fmaf(dxv[k], dy[w][k], incf);
+        const T inc = (T)incf * inv_factor;
+        const T inc2 = inc * inc;
+        if (s1) {
+          A[w] = (T)1 + (T)0.5 * inc + (T)(1.0 / 12) * inc2;
+          B[w] = (T)1 - (T)(1.0 / 12) * inc2;
+        } else {
+          A[w] = inc;  // hybrid diagonal cells need inc
+          B[w] = inc - (T)1;
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < REP; ++r) {
+        const int i = ci * REP + r;
+        T lft = left[r];
+        T cor = r == 0 ? corner_prev : left[r - 1];
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          const int c = lane * W + w;
+          const T upw = up[w];
+          T kn;
+          if (s1) {
+            kn = (upw + lft) * A[w / REP] - cor * B[w / REP];
+          } else if (hybrid && c == i) {
+            const T inc = A[w / REP], inc2 = inc * inc;
+            kn = (upw + lft) * ((T)1 + (T)0.5 * inc + (T)(1.0 / 12) * inc2) - cor * ((T)1 - (T)(1.0 / 12) * inc2);
+          } else {
+            kn = (upw + lft) + cor * B[w / REP];
+          }
+          if (c < J) {
+            cor = upw;
+            lft = kn;
+            up[w] = kn;
+          }
+        }
+        last[r] = lft;
+      }
+    }
+    corner_prev = left[REP - 1];
+  }
+  const int owner = (J - 1) / W, slot = (J - 1) % W;
+  T res = (T)0;
+#pragma unroll
+  for (int w = 0; w < W; ++w)
+    if (w == slot) res = up[w];
+  if (lane == owner) {
+    const float v = (float)res;
+    if (p.pair_mode == GPSIG_PAIRS_DIAG) {
+      p.out[a] = v;
+    } else {
+      if (a >= p.out_row0 && a < p.out_row0 + p.out_rows) p.out[(long long)(a - p.out_row0) * p.out_ld + b] = v;
+      if (p.pair_mode == GPSIG_PAIRS_UPPER && a != b && b >= p.out_row0 && b < p.out_row0 + p.out_rows)
+        p.out[(long long)(b - p.out_row0) * p.out_ld + a] = v;
+    }
+  }
+}
+
+template <typename T, int DP, int W, int REP>
+static int launch_pde_rep(const PdeArgs &a, long long nblocks, hipStream_t s) {
+  if constexpr ((W / REP) * DP > 64) {
+    return -1;  // the per-row kernel keeps fewer increments in registers
+  }
+  const size_t lds = (size_t)4 * (a.l1 - 1) * DP * sizeof(float);
+  if (lds > 64 * 1024) return GPSIG_EUNSUPPORTED;
+  hipLaunchKernelGGL((pde_rep_kernel<T, DP, W, REP>), dim3((unsigned)nblocks), dim3(256), lds, s, a);
+  return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
+}
+
+// W = the smallest multiple of REP with J / W <= 64 lanes (-1: use the per-row kernel)
+template <typename T, int DP, int REP>
+static int pde_rep_w(const PdeArgs &a, long long nblocks, int J, hipStream_t s) {
+  if (J <= 64 * REP) return launch_pde_rep<T, DP, REP, REP>(a, nblocks, s);
+  if (J <= 128 * REP && 2 * REP <= 16) return launch_pde_rep<T, DP, (2 * REP <= 16 ? 2 * REP : REP), REP>(a, nblocks, s);
+  if (REP <= 4 && J <= 192 * REP) return launch_pde_rep<T, DP, (REP <= 4 ? 3 * REP : REP), REP>(a, nblocks, s);
+  if (REP <= 4 && J <= 256 * REP) return launch_pde_rep<T, DP, (REP <= 4 ? 4 * REP : REP), REP>(a, nblocks, s);
+  return -1;
+}
+
 template <typename T, int DP, int W>
 static int launch_pde(const PdeArgs &a, long long nblocks, hipStream_t s) {
   if constexpr (W * DP > 128) {
@@ -162,6 +329,13 @@ static int launch_pde(const PdeArgs &a, long long nblocks, hipStream_t s) {
 
 template <typename T, int DP>
 static int pde_w(const PdeArgs &a, long long nblocks, int J, hipStream_t s) {
+  {
+    int rc = -1;
+    if (a.dyadic == 0) rc = pde_rep_w<T, DP, 1>(a, nblocks, J, s);
+    if (a.dyadic == 1) rc = pde_rep_w<T, DP, 2>(a, nblocks, J, s);
+    if (a.dyadic == 2) rc = pde_rep_w<T, DP, 4>(a, nblocks, J, s);
+    if (rc != -1) return rc;
+  }
   if (J <= 64) return launch_pde<T, DP, 1>(a, nblocks, s);
   if (J <= 128) return launch_pde<T, DP, 2>(a, nblocks, s);
   if (J <= 256) return launch_pde<T, DP, 4>(a, nblocks, s);

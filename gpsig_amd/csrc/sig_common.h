@@ -239,7 +239,7 @@ struct RbfSeedPk {
     for (int w2 = 0; w2 < W2; ++w2)
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        const int j = gl * W + 2 * w2 + h;
+        const int j = gl * W + w2 + h * W2;  // pair w2 = columns (w2, w2 + W/2) of the lane
         const int jj = j < l2 ? j : l2 - 1;
         const float *f = fy + (long long)jj * FS;
 #pragma unroll
@@ -335,9 +335,9 @@ struct RbfSeedPk {
       // corner difference k11 - k10 - k01 + k00 for the cells outside the polynomial range
 #pragma unroll
       for (int w = 0; w < W; ++w) {
-        const int w2 = w / 2, h = w % 2;
-        const float kn1 = (w + 1 < W) ? kn[(w + 1) / 2][(w + 1) % 2] : knR;
-        const float kc1 = (w + 1 < W) ? kc[(w + 1) / 2][(w + 1) % 2] : kcR;
+        const int w2 = w % W2, h = w / W2;
+        const float kn1 = (w + 1 < W) ? kn[(w + 1) % W2][(w + 1) / W2] : knR;
+        const float kc1 = (w + 1 < W) ? kc[(w + 1) % W2][(w + 1) / W2] : kcR;
         const float naive = (kn1 - kn[w2][h]) - (kc1 - kc[w2][h]);
         const float m = __builtin_fmaxf(__builtin_fabsf(p[w2][h]), __builtin_fabsf(c[w2][h]));
         float v = m < EM1_TAU ? dM[w2][h] : naive;

@@ -88,31 +88,33 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
       float d1[W];
       seed.template row<true>(rd, d1);
 #pragma unroll
-      for (int w2 = 0; w2 < W2; ++w2) dM[w2] = (f2){d1[2 * w2], d1[2 * w2 + 1]};
+      for (int w2 = 0; w2 < W2; ++w2) dM[w2] = (f2){d1[w2], d1[w2 + W2]};
     }
-    // lane totals of C_m (pair tree), scanned across the group for all M-1 levels together; then
-    // S_m(j) = (exclusive cross-lane prefix) + (exclusive in-lane prefix), written straight into
-    // the column pairs
+    // Column pair k of a lane holds columns (k, k + W/2), so the in-lane exclusive prefix runs on both
+    // halves at once: E_k = P_0 + ... + P_{k-1} (packed), E_{W/2} = (H_lo, H_hi) the half totals, and
+    // S_m(column) = E_k + (b, b + H_lo) with b the exclusive cross-lane prefix of T = H_lo + H_hi.
+    // The lane totals of the M-1 levels are scanned across the group together.
     constexpr int ML = M > 1 ? M - 1 : 1;
+    f2 E[ML][W2 + 1];
     float T[ML], base[ML];
 #pragma unroll
     for (int m = 0; m + 1 < M; ++m) {
-      f2 s2 = C[m][0];
+      E[m][1] = C[m][0];
 #pragma unroll
-      for (int w2 = 1; w2 < W2; ++w2) s2 += C[m][w2];
-      T[m] = s2[0] + s2[1];
+      for (int k = 2; k <= W2; ++k) E[m][k] = E[m][k - 1] + C[m][k - 1];
+      T[m] = E[m][W2][0] + E[m][W2][1];
       base[m] = T[m];
     }
     if constexpr (M > 1) group_incl_scan_n<LP, ML>(base);
-    // descending m: level m reads C_m before level m-1's update writes it
+    // descending m: level m reads C_m (through E) before level m-1's update writes it
 #pragma unroll
     for (int m = M - 2; m >= 0; --m) {
-      f2 S[W2];
-      S[0][0] = base[m] - T[m];
+      f2 off;
+      off[0] = base[m] - T[m];
+      off[1] = off[0] + E[m][W2][0];
+      C[m + 1][0] = fma2(dM[0], off, C[m + 1][0]);
 #pragma unroll
-      for (int w = 1; w < W; ++w) S[w / 2][w % 2] = S[(w - 1) / 2][(w - 1) % 2] + C[m][(w - 1) / 2][(w - 1) % 2];
-#pragma unroll
-      for (int w2 = 0; w2 < W2; ++w2) C[m + 1][w2] = fma2(dM[w2], S[w2], C[m + 1][w2]);
+      for (int k = 1; k < W2; ++k) C[m + 1][k] = fma2(dM[k], E[m][k] + off, C[m + 1][k]);
     }
 #pragma unroll
     for (int w2 = 0; w2 < W2; ++w2) C[0][w2] += dM[w2];
@@ -163,12 +165,19 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
 }
 
 // Column geometry: W columns per lane, LP lanes per pair; capacity LP*W >= points per sequence.
+// The lane keeps 2*W*DP column floats (y, dy) in VGPRs, so wide channel counts take fewer columns per
+// lane (more lanes per pair): W*DP <= 64 keeps the kernel within 256 VGPRs.
 struct Geo { int W, LP; };
-inline Geo fo_geometry(int l2) {
-  if (l2 <= 64) return {4, 16};
-  if (l2 <= 128) return {8, 16};
-  if (l2 <= 256) return {8, 32};
-  if (l2 <= 512) return {8, 64};
+__host__ __device__ constexpr int fo_wmax(int DP) { return DP <= 8 ? 8 : (DP <= 16 ? 4 : 2); }
+// longest sequences: W may exceed fo_wmax at LP = 64 (register spills, still correct)
+__host__ __device__ constexpr int fo_wcap(int DP) { return DP <= 16 ? 8 : 4; }
+inline Geo fo_geometry(int l2, int DP) {
+  // smallest LP (shortest scans) at which some W <= fo_wmax covers the sequence, smallest such W
+  for (int LP : {16, 32, 64})
+    for (int W = 2; W <= fo_wmax(DP); W *= 2)
+      if (LP * W >= l2) return {W, LP};
+  for (int W = 2 * fo_wmax(DP); W <= fo_wcap(DP); W *= 2)
+    if (64 * W >= l2) return {W, 64};
   return {0, 0};
 }
 constexpr int FO_MAX_LEVELS = 8;
@@ -185,11 +194,16 @@ int launch_fo(const SigArgs &a, long long nblocks, hipStream_t s) {
 
 template <int DP, int M, int SEED>
 int fo_geo(const SigArgs &a, long long nblocks, hipStream_t s) {
-  const Geo geo = fo_geometry(a.l2);
-  if (geo.W == 4 && geo.LP == 16) return launch_fo<DP, 4, 16, M, SEED>(a, nblocks, s);
-  if (geo.W == 8 && geo.LP == 16) return launch_fo<DP, 8, 16, M, SEED>(a, nblocks, s);
-  if (geo.W == 8 && geo.LP == 32) return launch_fo<DP, 8, 32, M, SEED>(a, nblocks, s);
-  if (geo.W == 8 && geo.LP == 64) return launch_fo<DP, 8, 64, M, SEED>(a, nblocks, s);
+  const Geo geo = fo_geometry(a.l2, DP);
+  constexpr int WM = fo_wmax(DP), WC = fo_wcap(DP);
+#define GPSIG_GEO(w, lp) \
+  if (geo.W == w && geo.LP == lp) return launch_fo<DP, w, lp, M, SEED>(a, nblocks, s);
+  GPSIG_GEO(2, 16) GPSIG_GEO(2, 32) GPSIG_GEO(2, 64)
+  if constexpr (WM >= 4) { GPSIG_GEO(4, 16) GPSIG_GEO(4, 32) }
+  if constexpr (WC >= 4) { GPSIG_GEO(4, 64) }
+  if constexpr (WM >= 8) { GPSIG_GEO(8, 16) GPSIG_GEO(8, 32) }
+  if constexpr (WC >= 8) { GPSIG_GEO(8, 64) }
+#undef GPSIG_GEO
   return GPSIG_EUNSUPPORTED;
 }
 
