@@ -153,7 +153,7 @@ __global__ __launch_bounds__(256) void pde_kernel(PdeArgs p) {
 // evaluates the lane's W/REP coarse increments and update coefficients once and then sweeps REP fine
 // rows x W fine columns; the skew is one step per coarse row, the left boundary of the REP rows comes
 // from lane l-1 (REP DPP moves per step).
-template <typename T, int DP, int W, int REP>
+template <typename T, int DP, int W, int REP, int SOLVER>
 __global__ __launch_bounds__(256) void pde_rep_kernel(PdeArgs p) {
   static_assert(W % REP == 0, "a lane owns whole coarse columns");
   constexpr int WC = W / REP;
@@ -207,8 +207,8 @@ __global__ __launch_bounds__(256) void pde_rep_kernel(PdeArgs p) {
   __syncthreads();
   if (!ok) return;
 
-  const bool hybrid = (p.pair_mode == GPSIG_PAIRS_DIAG) && p.solver == 0;
-  const bool s1 = p.solver == 1;
+  const bool hybrid = (p.pair_mode == GPSIG_PAIRS_DIAG) && SOLVER == 0;
+  constexpr bool s1 = SOLVER == 1;
   T up[W];
 #pragma unroll
   for (int w = 0; w < W; ++w) up[w] = (T)1;
@@ -240,7 +240,7 @@ __global__ __launch_bounds__(256) void pde_rep_kernel(PdeArgs p) {
         for (int k = 0; k < DP; ++k) incf = __builtin_fmaf(dxv[k], dy[w][k], incf);
         const T inc = (T)incf * inv_factor;
         const T inc2 = inc * inc;
-        if (s1) {
+        if constexpr (s1) {
           A[w] = (T)1 + (T)0.5 * inc + (T)(1.0 / 12) * inc2;
           B[w] = (T)1 - (T)(1.0 / 12) * inc2;
         } else {
@@ -253,24 +253,25 @@ __global__ __launch_bounds__(256) void pde_rep_kernel(PdeArgs p) {
         const int i = ci * REP + r;
         T lft = left[r];
         T cor = r == 0 ? corner_prev : left[r - 1];
+        // Columns c >= J (padding of the lane straddling J, and lanes past it) are updated too: the
+        // solution only flows right and down, so they never reach a real cell, and the lane's last
+        // column hands its value only to lanes that are all padding.
 #pragma unroll
         for (int w = 0; w < W; ++w) {
-          const int c = lane * W + w;
           const T upw = up[w];
           T kn;
-          if (s1) {
+          if constexpr (s1) {
             kn = (upw + lft) * A[w / REP] - cor * B[w / REP];
-          } else if (hybrid && c == i) {
-            const T inc = A[w / REP], inc2 = inc * inc;
-            kn = (upw + lft) * ((T)1 + (T)0.5 * inc + (T)(1.0 / 12) * inc2) - cor * ((T)1 - (T)(1.0 / 12) * inc2);
           } else {
             kn = (upw + lft) + cor * B[w / REP];
+            if (hybrid && lane * W + w == i) {
+              const T inc = A[w / REP], inc2 = inc * inc;
+              kn = (upw + lft) * ((T)1 + (T)0.5 * inc + (T)(1.0 / 12) * inc2) - cor * ((T)1 - (T)(1.0 / 12) * inc2);
+            }
           }
-          if (c < J) {
-            cor = upw;
-            lft = kn;
-            up[w] = kn;
-          }
+          cor = upw;
+          lft = kn;
+          up[w] = kn;
         }
         last[r] = lft;
       }
@@ -298,11 +299,15 @@ template <typename T, int DP, int W, int REP>
 static int launch_pde_rep(const PdeArgs &a, long long nblocks, hipStream_t s) {
   if constexpr ((W / REP) * DP > 64) {
     return -1;  // the per-row kernel keeps fewer increments in registers
+  } else {
+    const size_t lds = (size_t)4 * (a.l1 - 1) * DP * sizeof(float);
+    if (lds > 64 * 1024) return GPSIG_EUNSUPPORTED;
+    if (a.solver == 1)
+      hipLaunchKernelGGL((pde_rep_kernel<T, DP, W, REP, 1>), dim3((unsigned)nblocks), dim3(256), lds, s, a);
+    else
+      hipLaunchKernelGGL((pde_rep_kernel<T, DP, W, REP, 0>), dim3((unsigned)nblocks), dim3(256), lds, s, a);
+    return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
   }
-  const size_t lds = (size_t)4 * (a.l1 - 1) * DP * sizeof(float);
-  if (lds > 64 * 1024) return GPSIG_EUNSUPPORTED;
-  hipLaunchKernelGGL((pde_rep_kernel<T, DP, W, REP>), dim3((unsigned)nblocks), dim3(256), lds, s, a);
-  return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
 }
 
 // W = the smallest multiple of REP with J / W <= 64 lanes (-1: use the per-row kernel)
