@@ -53,7 +53,7 @@ SIGNATURES = {
     "gpsig_tens_gram": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P]),
     "gpsig_rescaled": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _P, _P, _SZ, _P]),
     "gpsig_rescaled_workspace_bytes": (_SZ, [_I, _I]),
-    "gpsig_tens_workspace_bytes": (_SZ, [_I, _I, _I]),
+    "gpsig_tens_workspace_bytes": (_SZ, [_I, _I, _I, _I, _I]),
     "gpsig_version": (ctypes.c_char_p, []),
 }
 

@@ -23,18 +23,19 @@ __global__ __launch_bounds__(256) void tvs_features_kernel(const float *__restri
   const int s = (int)(idx / l), i = (int)(idx % l);
   const float *x = X + idx * d;
   const int FC = 2 * d + 3;
-  float hdx = 0.f, xdx = 0.f, hx = 0.f;
+  float hdx = 0.f, hx = 0.f;
+  double xdx = 0.0;  // g = <x, dx> + |dx|^2/2 accumulated in fp64, rounded once
   for (int k = 0; k < d; ++k) {
     const float xv = x[k];
     const float dv = (i + 1 < l) ? x[d + k] - xv : 0.0f;
     Ft[((long long)i * FC + k) * n + s] = xv;
     Ft[((long long)i * FC + d + k) * n + s] = dv;
     hdx = __builtin_fmaf(dv, dv, hdx);
-    xdx = __builtin_fmaf(xv, dv, xdx);
+    xdx = __builtin_fma((double)xv, (double)dv, xdx);
     hx = __builtin_fmaf(xv, xv, hx);
   }
   Ft[((long long)i * FC + 2 * d) * n + s] = 0.5f * hdx;
-  Ft[((long long)i * FC + 2 * d + 1) * n + s] = xdx + 0.5f * hdx;
+  Ft[((long long)i * FC + 2 * d + 1) * n + s] = (float)(xdx + 0.5 * (double)hdx);
   Ft[((long long)i * FC + 2 * d + 2) * n + s] = 0.5f * hx;
 }
 
@@ -512,8 +513,18 @@ using namespace gpsig;
 
 static int dpad4(int d) { return d <= 4 ? 4 : d <= 8 ? 8 : d <= 16 ? 16 : d <= 32 ? 32 : 0; }
 
-extern "C" size_t gpsig_tens_workspace_bytes(int n, int l, int d) {
+namespace gpsig {
+int tvs_pk_launch(const float *Z, int lt, int t, int increments, int d, const float *Ft, int n, int l, int M,
+                  float *out, float *Zp, hipStream_t s);
+size_t tvs_pk_zp_bytes(int lt, int t, int d);
+}  // namespace gpsig
+
+static size_t tvs_ft_bytes(int n, int l, int d) {
   return ((size_t)n * l * (2 * d + 3) * sizeof(float) + 255) & ~(size_t)255;
+}
+
+extern "C" size_t gpsig_tens_workspace_bytes(int n, int l, int d, int lt, int t) {
+  return tvs_ft_bytes(n, l, d) + tvs_pk_zp_bytes(lt, t, d);
 }
 
 extern "C" int gpsig_tens_vs_seq(const float *Z, int lt, int t, int increments, int d, const float *X, int n, int l,
@@ -526,10 +537,15 @@ extern "C" int gpsig_tens_vs_seq(const float *Z, int lt, int t, int increments, 
   if (base_kind != GPSIG_BASE_RBF && base_kind != GPSIG_BASE_LINEAR) return GPSIG_EUNSUPPORTED;
   const int DP = dpad4(d);
   if (DP == 0) return GPSIG_EUNSUPPORTED;
-  if (!workspace || workspace_bytes < gpsig_tens_workspace_bytes(n, l, d)) return GPSIG_EWORKSPACE;
+  if (!workspace || workspace_bytes < gpsig_tens_workspace_bytes(n, l, d, lt, t)) return GPSIG_EWORKSPACE;
   float *Ft = static_cast<float *>(workspace);
   const long long tot = (long long)n * l;
   hipLaunchKernelGGL(tvs_features_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, X, n, l, d, Ft);
+  if (base_kind == GPSIG_BASE_RBF && difference && order == 1) {
+    float *Zp = reinterpret_cast<float *>(static_cast<char *>(workspace) + tvs_ft_bytes(n, l, d));
+    const int rc = tvs_pk_launch(Z, lt, t, increments, d, Ft, n, l, num_levels, out, Zp, s);
+    if (rc != -1) return rc;
+  }
   TvsArgs a{Z, Ft, lt, t, n, l, d, num_levels, order, increments, difference, base_kind == GPSIG_BASE_RBF, out};
   dim3 grid((n + 63) / 64, t);
   const size_t lds = (size_t)2 * 64 * lt * sizeof(float);

@@ -1,0 +1,260 @@
+// gpsig_amd -- fast path of gpsig_tens_vs_seq on gfx950: RBF base kernel, difference=True, order 1,
+// d <= 8, num_levels <= 6 (signature_algs.py:101-127 with the seeds of kernels.py:314-341).
+//
+// One wave per (tensor t, 128 sequences): each lane carries TWO sequences as the halves of packed
+// fp32 pairs (v_pk_* instructions), the tensor's components are wave-uniform SGPR operands.  Each
+// lane streams its sequences in time; per component k and time cell the seed is the time difference
+// of the base kernel, evaluated without cancellation and without an exp:
+//   M = k(z, x_{s+1}) - k(z, x_s) = k(z, x_s) expm1(q),  q = <z, dx_s> - g_s   (g_s = <x_s,dx_s> + |dx_s|^2/2)
+//   k(z, x_{s+1}) = k(z, x_s) + M                                              (row recurrence)
+// and with increments (component = (z0, z1), seed = time difference of k(z1, x) - k(z0, x)):
+//   M = k(z0, x_s) (Ep Eq + (1 + Ep)(1 + Eq) Ec),  p = -<z0 - x_s, dz> - |dz|^2/2,  q = <z0, dx_s> - g_s,
+//   c = <dz, dx_s>;   k(z0, x_{s+1}) = k(z0, x_s)(1 + Eq),  Ep_{s+1} = Ep + Ec + Ep Ec.
+// k (and Ep) are re-evaluated exactly every ANCHOR cells.  Arguments past the polynomial range take
+// expm1 = e^x - 1 (a wave-uniform branch); with increments, |q| or |c| >= 2 (far-apart corners) takes
+// the plain corner difference of directly evaluated base-kernel values.
+#include "sig_common.h"
+
+namespace gpsig {
+
+struct TvsPkArgs {
+  const float *Zp;  // (T, LT, ZS) prepared components: z (DP) | or z0 (DP), dz (DP), |dz|^2/2
+  const float *Ft;  // time-major features Ft[(s * FC + c) * n + seq], FC = 2d + 3 (sig_tens.hip)
+  int t, n, l, d;
+  float *out;       // (M+1, T, n)
+};
+
+template <int DP, bool INCR>
+__host__ __device__ constexpr int tvs_zs() { return INCR ? ((2 * DP + 1 + 1) & ~1) : DP; }
+
+// Zp[(tt * LT + k) * ZS + .] from Z (LT, T, d) or (LT, T, 2, d)
+template <int DP, bool INCR>
+__global__ __launch_bounds__(256) void tvs_prep_kernel(const float *__restrict__ Z, int lt, int t, int d,
+                                                       float *__restrict__ Zp) {
+  const int idx = blockIdx.x * 256 + threadIdx.x;
+  if (idx >= lt * t) return;
+  const int k = idx % lt, tt = idx / lt;
+  constexpr int ZS = tvs_zs<DP, INCR>();
+  float *o = Zp + (long long)(tt * lt + k) * ZS;
+  if (!INCR) {
+    const float *z = Z + ((long long)k * t + tt) * d;
+    for (int q = 0; q < DP; ++q) o[q] = q < d ? z[q] : 0.f;
+  } else {
+    const float *z = Z + (((long long)k * t + tt) * 2) * d;
+    float h = 0.f;
+    for (int q = 0; q < DP; ++q) {
+      const float z0 = q < d ? z[q] : 0.f, dz = q < d ? z[d + q] - z[q] : 0.f;
+      o[q] = z0;
+      o[DP + q] = dz;
+      h = __builtin_fmaf(dz, dz, h);
+    }
+    o[2 * DP] = 0.5f * h;
+    for (int q = 2 * DP + 1; q < ZS; ++q) o[q] = 0.f;
+  }
+}
+
+template <int DP, int M, bool INCR>
+__global__ __launch_bounds__(64) void tvs_pk_kernel(TvsPkArgs a) {
+  constexpr int LT = M * (M + 1) / 2;
+  constexpr int ZS = tvs_zs<DP, INCR>();
+  constexpr int ANCHOR = 8;
+  constexpr float TVS_CORNER = 2.0f;  // |q| or |c| past this: corner form (increments)
+  constexpr float NHL2E = -0.72134752044448170f, L2E = 1.4426950408889634f;
+  const int lane = threadIdx.x;
+  const int tt = blockIdx.y;
+  const int n = a.n, d = a.d, FC = 2 * d + 3;
+  const int s0 = blockIdx.x * 128 + lane, s1 = s0 + 64;
+  const int c0 = s0 < n ? s0 : n - 1, c1 = s1 < n ? s1 : n - 1;
+  const float *__restrict__ zp = a.Zp + (long long)tt * LT * ZS;
+
+  // loads of channel c of cell s for both sequences of the lane
+  auto ld = [&](int s, int c) {
+    const float *f = a.Ft + ((long long)s * FC + c) * n;
+    return (f2){f[c0], f[c1]};
+  };
+  auto ldx = [&](int s, f2 (&x)[DP]) {
+#pragma unroll
+    for (int q = 0; q < DP; ++q) x[q] = q < d ? ld(s, q) : splat2(0.f);
+  };
+  // exact k(z0_k, x) and (INCR) expm1(p_k) for the point x
+  auto exact = [&](int k, const f2 (&x)[DP], f2 &kck, f2 &Epk) {
+    const float *z = zp + k * ZS;
+    f2 s2 = splat2(0.f), pp = splat2(0.f);
+#pragma unroll
+    for (int q = 0; q < DP; ++q) {
+      const f2 df = splat2(z[q]) - x[q];
+      s2 = fma2(df, df, s2);
+      if constexpr (INCR) pp = fma2(df, splat2(-z[DP + q]), pp);
+    }
+    s2 = s2 * splat2(NHL2E);
+    kck[0] = __builtin_amdgcn_exp2f(s2[0]);
+    kck[1] = __builtin_amdgcn_exp2f(s2[1]);
+    if constexpr (INCR) {
+      pp = pp - splat2(z[2 * DP]);
+      Epk = em1_small2(pp);
+#pragma unroll
+      for (int h = 0; h < 2; ++h)
+        if (!(__builtin_fabsf(pp[h]) < EM1_TAU)) Epk[h] = __builtin_amdgcn_exp2f(pp[h] * L2E) - 1.0f;
+    }
+  };
+
+  f2 kc[LT], Ep[LT], Ss[LT], K[M + 1];
+#pragma unroll
+  for (int k = 0; k < LT; ++k) Ss[k] = splat2(0.f);
+#pragma unroll
+  for (int i = 0; i <= M; ++i) K[i] = splat2(0.f);
+  {
+    f2 x0[DP];
+    ldx(0, x0);
+#pragma unroll
+    for (int k = 0; k < LT; ++k) exact(k, x0, kc[k], Ep[k]);
+  }
+
+  const int ncell = a.l - 1;
+  for (int s = 0; s < ncell; ++s) {
+    // keeps the component loads inside the loop (hoisted, LT x ZS of them would not fit in SGPRs)
+    asm volatile("" ::: "memory");
+    f2 dx[DP];
+#pragma unroll
+    for (int q = 0; q < DP; ++q) dx[q] = q < d ? ld(s, d + q) : splat2(0.f);
+    const f2 g = ld(s, 2 * d + 1);
+    const bool anch = (s % ANCHOR) == ANCHOR - 1;
+    f2 x1[DP];
+    if (anch) ldx(s + 1, x1);
+    // components in (level, stage) order; the order-1 recursion (signature_algs.py:115-127) is folded
+    // in as each seed is produced
+#pragma unroll
+    for (int i = 1; i <= M; ++i) {
+      const int k0 = i * (i - 1) / 2;
+      f2 prev = splat2(0.f);
+#pragma unroll
+      for (int st = 0; st < i; ++st) {
+        const int k = k0 + st;
+        const float *z = zp + k * ZS;
+        f2 qv = -g, cv = splat2(0.f);
+#pragma unroll
+        for (int q = 0; q < DP; ++q) {
+          qv = fma2(dx[q], splat2(z[q]), qv);
+          if constexpr (INCR) cv = fma2(dx[q], splat2(z[DP + q]), cv);
+        }
+        float mx = __builtin_fmaxf(__builtin_fabsf(qv[0]), __builtin_fabsf(qv[1]));
+        if constexpr (INCR) mx = __builtin_fmaxf(mx, __builtin_fmaxf(__builtin_fabsf(cv[0]), __builtin_fabsf(cv[1])));
+        f2 Eq = em1_small2(qv), Ec = splat2(0.f);
+        if constexpr (INCR) Ec = em1_small2(cv);
+        const bool wide = __builtin_amdgcn_ballot_w64(mx >= EM1_TAU) != 0;
+        if (wide) {
+          // arguments past the polynomial range: expm1 = e^x - 1 (no cancellation there)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            if (!(__builtin_fabsf(qv[h]) < EM1_TAU)) Eq[h] = __builtin_amdgcn_exp2f(qv[h] * L2E) - 1.0f;
+            if constexpr (INCR)
+              if (!(__builtin_fabsf(cv[h]) < EM1_TAU)) Ec[h] = __builtin_amdgcn_exp2f(cv[h] * L2E) - 1.0f;
+          }
+        }
+        f2 m;
+        if constexpr (INCR) {
+          f2 t = fma2(Ep[k], Ec, Ec);
+          t = fma2(Eq, t, t);
+          m = kc[k] * fma2(Ep[k], Eq, t);
+        } else {
+          m = kc[k] * Eq;  // = k(z, x_{s+1}) - k(z, x_s) exactly, any q
+        }
+        if (INCR && wide && __builtin_amdgcn_ballot_w64(mx >= TVS_CORNER) != 0) {
+          // increments far apart: corner differences of directly evaluated base-kernel values
+          f2 xs[DP], xn[DP], kn, Epn;
+          ldx(s, xs);
+          ldx(s + 1, xn);
+          exact(k, xn, kn, Epn);
+          const float *z = zp + k * ZS;
+          f2 e1 = splat2(0.f), e0 = splat2(0.f);  // |z1 - x_{s+1}|^2, |z1 - x_s|^2
+#pragma unroll
+          for (int q = 0; q < DP; ++q) {
+            const f2 z1 = splat2(z[q] + z[DP + q]);
+            const f2 d1 = z1 - xn[q], d0 = z1 - xs[q];
+            e1 = fma2(d1, d1, e1);
+            e0 = fma2(d0, d0, e0);
+          }
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const bool ok = __builtin_fabsf(qv[h]) < TVS_CORNER && __builtin_fabsf(cv[h]) < TVS_CORNER;
+            const float k11 = __builtin_amdgcn_exp2f(e1[h] * NHL2E), k10 = __builtin_amdgcn_exp2f(e0[h] * NHL2E);
+            m[h] = ok ? m[h] : (k11 - k10) - (kn[h] - kc[k][h]);
+          }
+          kc[k] = kn;
+          Ep[k] = Epn;
+        } else if (anch) {
+          exact(k, x1, kc[k], Ep[k]);  // re-anchor the recurrences every ANCHOR cells
+        } else if constexpr (INCR) {
+          kc[k] = fma2(kc[k], Eq, kc[k]);
+          Ep[k] = fma2(Ep[k], Ec, Ep[k] + Ec);
+        } else {
+          kc[k] = kc[k] + m;
+        }
+        if (st == 0) {
+          prev = m;
+        } else {
+          const f2 ss = Ss[k - 1];
+          Ss[k - 1] = ss + prev;
+          prev = m * ss;
+        }
+      }
+      K[i] += prev;
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int sq = h ? s1 : s0;
+    if (sq < n) {
+      a.out[(long long)tt * n + sq] = 1.0f;
+#pragma unroll
+      for (int i = 1; i <= M; ++i) a.out[((long long)i * a.t + tt) * n + sq] = K[i][h];
+    }
+  }
+}
+
+template <int DP, int M, bool INCR>
+static int launch_tvs_pk(const float *Z, int lt, int t, int d, const float *Ft, int n, int l, float *out, float *Zp,
+                         hipStream_t s) {
+  hipLaunchKernelGGL((tvs_prep_kernel<DP, INCR>), dim3((unsigned)((lt * t + 255) / 256)), dim3(256), 0, s, Z, lt, t, d,
+                     Zp);
+  TvsPkArgs a{Zp, Ft, t, n, l, d, out};
+  hipLaunchKernelGGL((tvs_pk_kernel<DP, M, INCR>), dim3((unsigned)((n + 127) / 128), (unsigned)t), dim3(64), 0, s, a);
+  return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
+}
+
+template <int DP, bool INCR>
+static int tvs_pk_m(int M, const float *Z, int lt, int t, int d, const float *Ft, int n, int l, float *out, float *Zp,
+                    hipStream_t s) {
+  switch (M) {
+    case 1: return launch_tvs_pk<DP, 1, INCR>(Z, lt, t, d, Ft, n, l, out, Zp, s);
+    case 2: return launch_tvs_pk<DP, 2, INCR>(Z, lt, t, d, Ft, n, l, out, Zp, s);
+    case 3: return launch_tvs_pk<DP, 3, INCR>(Z, lt, t, d, Ft, n, l, out, Zp, s);
+    case 4: return launch_tvs_pk<DP, 4, INCR>(Z, lt, t, d, Ft, n, l, out, Zp, s);
+    case 5: return launch_tvs_pk<DP, 5, INCR>(Z, lt, t, d, Ft, n, l, out, Zp, s);
+    case 6: return launch_tvs_pk<DP, 6, INCR>(Z, lt, t, d, Ft, n, l, out, Zp, s);
+    default: return -1;
+  }
+}
+
+// -1: not covered by the fast path (the caller runs the general kernel)
+int tvs_pk_launch(const float *Z, int lt, int t, int increments, int d, const float *Ft, int n, int l, int M,
+                  float *out, float *Zp, hipStream_t s) {
+  if (M > 6 || d > 8 || l < 2) return -1;
+  const int DP = d <= 2 ? 2 : d <= 4 ? 4 : d <= 6 ? 6 : 8;
+#define GPSIG_TVS(dp)                                                               \
+  case dp:                                                                          \
+    return increments ? tvs_pk_m<dp, true>(M, Z, lt, t, d, Ft, n, l, out, Zp, s)    \
+                      : tvs_pk_m<dp, false>(M, Z, lt, t, d, Ft, n, l, out, Zp, s);
+  switch (DP) {
+    GPSIG_TVS(2) GPSIG_TVS(4) GPSIG_TVS(6) GPSIG_TVS(8)
+    default: return -1;
+  }
+#undef GPSIG_TVS
+}
+
+size_t tvs_pk_zp_bytes(int lt, int t, int d) {
+  const int DP = d <= 2 ? 2 : d <= 4 ? 4 : d <= 6 ? 6 : 8;
+  return ((size_t)lt * t * ((2 * DP + 2)) * sizeof(float) + 255) & ~(size_t)255;
+}
+
+}  // namespace gpsig

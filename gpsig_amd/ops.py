@@ -178,7 +178,7 @@ def tens_vs_seq(Z: torch.Tensor, X: torch.Tensor, num_levels: int, order: int = 
     if lt != num_levels * (num_levels + 1) // 2:
         raise ValueError(f"Z must have num_levels*(num_levels+1)/2 = {num_levels * (num_levels + 1) // 2} components")
     out = torch.empty((num_levels + 1, t, n), dtype=torch.float32, device=X.device)
-    ws = workspace(X.device, lib.gpsig_tens_workspace_bytes(n, l, d))
+    ws = workspace(X.device, lib.gpsig_tens_workspace_bytes(n, l, d, lt, t))
     rc = lib.gpsig_tens_vs_seq(Z.data_ptr(), lt, t, int(increments), d, X.data_ptr(), n, l, num_levels, order,
                                base_kind(base), int(difference), out.data_ptr(), ws.data_ptr(), ws.numel(),
                                _stream(X.device))

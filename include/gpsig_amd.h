@@ -104,7 +104,8 @@ int gpsig_sig_diag(const float *X, int n, int l, int d, int num_levels, int orde
  * (signature_algs_vosf.py:11-48): <S(x_n), (I - Lambda_t) S(x_n)> per level with Lambda_t the rank-1
  * diagonal built from Z (LT, T, d).  out (num_levels+1, n, T).
  */
-size_t gpsig_tens_workspace_bytes(int n, int l, int d);
+/* Workspace of gpsig_tens_vs_seq for n sequences of l points in d channels and lt x t components. */
+size_t gpsig_tens_workspace_bytes(int n, int l, int d, int lt, int t);
 
 int gpsig_tens_vs_seq(const float *Z, int lt, int t, int increments, int d, const float *X, int n, int l,
                       int num_levels, int order, int base_kind, int difference, float *out, void *workspace,
