@@ -85,10 +85,12 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--workload", default="H", choices=sorted(WORKLOADS))
-    ap.add_argument("--n", type=int)
+    ap.add_argument("--nseq", "--n", dest="n", type=int, help="override the workload N")
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--backend", default="nccl",
+                    help="process-group backend (nccl = RCCL; gloo only to rehearse N>1 ranks on one GPU)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r1_gram_counters.json"),
                     help="per-launch HBM bytes of the Gram kernel from a PMC pass (profiles/*.json)")
     args = ap.parse_args()
@@ -99,10 +101,13 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank % max(1, torch.cuda.device_count()))
+    torch.cuda.set_device(dev)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local_rank))
-    dev = torch.device("cuda", local_rank)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group(args.backend)
 
     import gpsig_amd
     from gpsig_amd import _lib as L
