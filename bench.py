@@ -198,7 +198,7 @@ def main():
                      "entries_per_launch": entries_per_launch,
                      # the fused kernel never materialises the tile: physically it is VALU-issue bound
                      "physical_bound": "valu", "valu_issue_util": prof.get("valu_issue_util"),
-                     "profile": args.traffic_json if prof else None},
+                     "profile": os.path.relpath(args.traffic_json, ROOT) if prof else None},
     }
     if rank == 0 and not args.no_check:
         # parity on a bounded subsample: the normalised Gram restricted to a subset S of the sequences

@@ -112,7 +112,7 @@ def row_pde(reps, cpu_s):
     ref = pde.pde_gram(Xnp[S].astype(np.float64), None, dy, 1)
     got = K[torch.as_tensor(S, device=dev)][:, torch.as_tensor(S, device=dev)].double().cpu().numpy()
     b_entry = 4 * (l - 1) ** 2 + 4
-    threads = len(os.sched_getaffinity(0))
+    threads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16")))
     Xc = Xnp[:16].astype(np.float64)
     cpu = cpu_rate(lambda: pde.pde_gram(Xc[:8], Xc[8:16], dy, 1), 64, cpu_s)
     return dict(config="C3", workload=f"PDE Gram K(X) N={n} L={l} D={d} dyadic={dy} solver=1 (fp64 solution)",
