@@ -46,6 +46,8 @@ SIGNATURES = {
     "gpsig_sig_gram": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I,
                             _P, _P, _P, _F, _I, _P, _I, _I, _P, _SZ, _P]),
     "gpsig_sig_diag": (_I, [_P, _I, _I, _I, _I, _I, _I, _I, _F, _I, _P, _P, _SZ, _P]),
+    "gpsig_sig_gram_vjp": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _I,
+                                _P, _P, _P, _F, _P, _P, _P, _P, _P, _P, _SZ, _P]),
     "gpsig_pde_gram": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _I, _I, _P]),
     "gpsig_pde_diag": (_I, [_P, _I, _I, _I, _I, _I, _P, _P]),
     "gpsig_sym_assemble": (_I, [_P, _P, ctypes.c_longlong, _I, _I, _P, _P]),

@@ -1,0 +1,97 @@
+"""torch.autograd bindings of the gfx950 Gram kernels.
+
+The reference differentiates SignatureKernel.K / Kdiag with TF autodiff through the materialised
+graph (gpsig/kernels.py:209-238, 402-477, 510-541; gpsig/signature_algs.py:8-35).  Here the forward
+is the fused Gram kernel and the backward is the gpsig_sig_gram_vjp kernel (gpsig_amd/csrc/sig_bwd.h):
+
+  K(X) / K(X, X2), normalised:  out = sum_m s_m (K_m + jitter [a == b]) rs_m(a) rs_m(b)
+    one VJP launch over the Gram pairs gives dLoss/dX, dLoss/dX2 through K_m, dLoss/drs and
+    dLoss/ds; dLoss/drs is chained through rs = (K_m(a, a) + jitter)^-1/2 into one VJP launch over the
+    diagonal pairs.
+
+Gradients reach the sequences (and, through the host-side scaling in kernels.py, the lengthscales)
+and sigma * variances.  Supported for order == 1 with difference == True (the reference defaults);
+other configurations evaluate forward but raise NotImplementedError on backward.
+"""
+from __future__ import annotations
+
+import torch
+
+from . import _lib as L
+from . import ops
+
+
+def _check_bwd(cfg):
+    if cfg["order"] != 1 or not cfg["difference"]:
+        raise NotImplementedError("gradients of the signature-kernel Gram are implemented for order=1 and "
+                                  "difference=True (gpsig_sig_gram_vjp)")
+
+
+class SigGram(torch.autograd.Function):
+    """Normalised / raw signature Gram (SignatureKernel.K) with a gfx950 backward."""
+
+    @staticmethod
+    def forward(ctx, Xs, X2s, scale, cfg):
+        M = cfg["num_levels"]
+        mode = L.OUT_NORM_LEVELS if cfg["return_levels"] else L.OUT_NORM_SUM
+        sc32 = scale.detach().to(torch.float32)
+        kw = dict(order=cfg["order"], base=cfg["base"], difference=cfg["difference"])
+        rs1 = rs2 = None
+        if cfg["normalization"]:
+            rs1 = ops.sig_diag(Xs.detach(), M, jitter=cfg["jitter"], rsqrt=True, **kw)
+            rs2 = rs1 if X2s is None else ops.sig_diag(X2s.detach(), M, jitter=cfg["jitter"], rsqrt=True, **kw)
+        jit = cfg["jitter"] if (cfg["normalization"] and X2s is None) else 0.0
+        out = ops.sig_gram(Xs.detach(), None if X2s is None else X2s.detach(), M, rs1=rs1, rs2=rs2, scale=sc32,
+                           jitter=jit, out_mode=mode, **kw)
+        ctx.cfg = cfg
+        ctx.scale_dtype = scale.dtype
+        ctx.save_for_backward(Xs, X2s, sc32, rs1, rs2)
+        return out
+
+    @staticmethod
+    def backward(ctx, gout):
+        cfg = ctx.cfg
+        _check_bwd(cfg)
+        Xs, X2s, sc32, rs1, rs2 = ctx.saved_tensors
+        M = cfg["num_levels"]
+        sym = X2s is None
+        dev = Xs.device
+        n1 = Xs.shape[0]
+        n2 = n1 if sym else X2s.shape[0]
+        grs1 = grs2 = None
+        if cfg["normalization"]:
+            grs1 = torch.zeros((M + 1, n1), dtype=torch.float32, device=dev)
+            grs2 = grs1 if sym else torch.zeros((M + 1, n2), dtype=torch.float32, device=dev)
+        gscale = torch.zeros((M + 1,), dtype=torch.float32, device=dev)
+        jit = cfg["jitter"] if (cfg["normalization"] and sym) else 0.0
+        gX, gY = ops.sig_gram_vjp(Xs.detach(), None if sym else X2s.detach(), M, gout, base=cfg["base"],
+                                  gout_levels=cfg["return_levels"], rs1=rs1, rs2=rs2, scale=sc32, jitter=jit,
+                                  grs1=grs1, grs2=grs2, gscale=gscale)
+        if cfg["normalization"]:
+            # rs = (K_m(a, a) + jitter)^-1/2  ->  dLoss/dK_m(a, a) = -rs^3/2 dLoss/drs
+            ops.sig_gram_vjp(Xs.detach(), None, M, grs1 * (-0.5) * rs1 ** 3, base=cfg["base"], diag=True, gX=gX)
+            if not sym:
+                ops.sig_gram_vjp(X2s.detach(), None, M, grs2 * (-0.5) * rs2 ** 3, base=cfg["base"], diag=True,
+                                 gX=gY)
+        gXo = gX.to(Xs.dtype) if ctx.needs_input_grad[0] else None
+        gYo = gY.to(X2s.dtype) if (not sym and ctx.needs_input_grad[1]) else None
+        gso = gscale.to(ctx.scale_dtype) if ctx.needs_input_grad[2] else None
+        return gXo, gYo, gso, None
+
+
+class SigDiag(torch.autograd.Function):
+    """Raw per-level diagonal k(x_a, x_a) (SignatureKernel._K_seq_diag) with a gfx950 backward."""
+
+    @staticmethod
+    def forward(ctx, Xs, cfg):
+        ctx.cfg = cfg
+        ctx.save_for_backward(Xs)
+        return ops.sig_diag(Xs.detach(), cfg["num_levels"], cfg["order"], cfg["base"], cfg["difference"])
+
+    @staticmethod
+    def backward(ctx, gout):
+        cfg = ctx.cfg
+        _check_bwd(cfg)
+        (Xs,) = ctx.saved_tensors
+        gX, _ = ops.sig_gram_vjp(Xs.detach(), None, cfg["num_levels"], gout, base=cfg["base"], diag=True)
+        return gX.to(Xs.dtype), None

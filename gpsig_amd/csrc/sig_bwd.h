@@ -1,0 +1,466 @@
+// gpsig_amd -- gradient (vector-Jacobian product) of the first-order signature-kernel Gram on gfx950.
+//
+// The reference differentiates K through TF autodiff of the materialised graph (kernels.py:209-238
+// base-kernel tensor -> signature_algs.py:8-35 recursion -> kernels.py:431-477 normalisation), keeping
+// every (N1, L1, N2, L2) intermediate alive for the backward pass.  Here one lane group owns one pair
+// (a, b) as in the forward kernel (sig_fo.h) and nothing grid-sized touches memory:
+//
+//   forward sweep  rows i = 0 .. L1-2:  C_m(j) += dM(i,j) S_{m-1}(i,j),  S_m = exclusive scan_j C_m
+//                  (the forward recursion; its end state gives K_m(a,b) for the normalisation term)
+//   reverse sweep  rows i = L1-2 .. 0:
+//     * the forward state of row i is recovered by inverting the update (C_m -= dM S_{m-1}, levels in
+//       ascending order), so no per-row state is stored;
+//     * adjoint of the column sums: Ch_m(i) = Ch_m(i+1) + reverse-exclusive-scan_j(dM(i,.) Ch_{m+1}(i+1,.)),
+//       Ch_m(L1-1) = g_m = dLoss/dK_m(a,b);
+//     * dLoss/d dM(i,j) = sum_m Ch_m(i+1,j) S_{m-1}(i,j);
+//     * the adjoint of the second difference (signature_algs.py:26) turns it into dLoss/dk(x_i, y_j) on
+//       the point grid, and the base kernel's derivative (RBF: k (y - x); linear: y) gives the point
+//       gradients: x-rows are reduced across the wave and added to gX, y-columns accumulate in lane
+//       registers and are added to gY at the end.
+//
+// Both sweeps evaluate each k(x_i, y_j) row with the same instructions (one exp per cell), so the
+// cells dM of the reverse sweep are bitwise those of the forward sweep and the inversion only carries
+// the fp32 rounding of the forward sums.
+#pragma once
+#include "sig_common.h"
+
+namespace gpsig {
+
+struct BwdArgs {
+  const float *FX, *FY;  // feature records (n1,l1,FS), (n2,l2,FS)
+  int n1, l1, n2, l2, d;
+  int M;
+  int pair_mode, row_begin, row_end;
+  int tiles_a0, ntb;
+  long long tile_base;
+  const float *gout;  // upstream gradient: (n1, n2) summed [levels == 0] or (M+1, n1, n2) per level;
+                      // DIAG: (M+1, n1)
+  int gout_levels;
+  long long g_ld, g_lvl;
+  const float *rs1, *rs2, *scale;
+  float jitter;
+  float *gX, *gY, *grs1, *grs2, *gscale;
+};
+
+// Exclusive scan over the group's columns of per-lane column arrays v[W] (W columns of lane gl hold
+// columns gl*W .. gl*W+W-1), N independent arrays, scans step-interleaved.
+template <int LP, int W, int N>
+GPSIG_DEV void group_excl_cols_n(const float (&v)[N][W], float (&out)[N][W]) {
+  float t[N], incl[N];
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    float s = 0.0f;
+#pragma unroll
+    for (int w = 0; w < W; ++w) s += v[n][w];
+    t[n] = s;
+    incl[n] = s;
+  }
+  group_incl_scan_n<LP, N>(incl);
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    float run = incl[n] - t[n];
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      out[n][w] = run;
+      run += v[n][w];
+    }
+  }
+}
+
+// Reverse exclusive scan (sum over columns j' > j of the group) of N arrays.
+template <int LP, int W, int N>
+GPSIG_DEV void group_rexcl_cols_n(const float (&v)[N][W], float (&out)[N][W]) {
+  float t[N], incl[N];
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    float s = 0.0f;
+#pragma unroll
+    for (int w = 0; w < W; ++w) s += v[n][w];
+    t[n] = s;
+    incl[n] = s;
+  }
+  group_incl_scan_n<LP, N>(incl);
+  const int last = (int)(__lane_id() | (LP - 1));
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    const float tot = __shfl(incl[n], last, 64);
+    float run = tot - incl[n];  // sum over the lanes after this one
+#pragma unroll
+    for (int w = W - 1; w >= 0; --w) {
+      out[n][w] = run;
+      run += v[n][w];
+    }
+  }
+}
+
+// Sum over the whole wave of N values; the result is valid in lane 63.
+template <int N>
+GPSIG_DEV void wave_sum_last_n(float (&v)[N]) {
+  group_incl_scan_n<64, N>(v);
+}
+
+template <int DP, int W, int LP, int M, int SEED>
+__global__ __launch_bounds__(256) void sig_bwd_kernel(BwdArgs p) {
+  constexpr int FS = feat_stride(DP);
+  constexpr int G = 64 / LP;
+  constexpr bool RBF = (SEED == SEED_RBF_DIFF);
+  constexpr float NHL2E = -0.72134752044448170f;  // exp(-d2/2) = exp2(d2 * NHL2E)
+  constexpr int ML = M > 1 ? M - 1 : 1;
+
+  const int lane = threadIdx.x & 63;
+  const int wave = wave_uniform(threadIdx.x >> 6);
+  const int g = lane / LP;
+  const int gl = lane % LP;
+  const bool diag = p.pair_mode == GPSIG_PAIRS_DIAG;
+
+  // ---- which pair (same enumeration as sig_fo_kernel)
+  int a, b;
+  if (diag) {
+    a = p.row_begin + (int)blockIdx.x * 4 + wave;
+    b = a;
+    if (a >= p.row_end) return;
+  } else {
+    int ta, tb;
+    if (p.pair_mode == GPSIG_PAIRS_UPPER) {
+      const Tile t = upper_tile(p.tile_base + (long long)blockIdx.x, p.ntb, 4 / G);
+      ta = t.ta;
+      tb = t.tb;
+    } else {
+      ta = p.tiles_a0 + (int)blockIdx.x / p.ntb;
+      tb = (int)blockIdx.x % p.ntb;
+    }
+    a = ta * 4 + wave;
+    b = tb * G + g;
+    if (a < p.row_begin || a >= p.row_end) return;  // wave-uniform
+  }
+  bool pair_ok = b < p.n2;
+  if (p.pair_mode == GPSIG_PAIRS_UPPER) pair_ok = pair_ok && b >= a;
+  if (diag) pair_ok = (g == 0);
+  const int bl = b < p.n2 ? b : p.n2 - 1;
+  const int l1 = p.l1, l2 = p.l2;
+
+  const float *__restrict__ fx = p.FX + (long long)a * l1 * FS;
+  const float *__restrict__ fy = p.FY + (long long)bl * l2 * FS;
+
+  // ---- column data of this lane
+  float y[W][DP], dy[W][DP], hdy[W];
+  bool colv[W], ptv[W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    const int j = gl * W + w;
+    colv[w] = j < l2 - 1;
+    ptv[w] = j < l2;
+    const int jj = j < l2 ? j : l2 - 1;
+    const float *f = fy + (long long)jj * FS;
+#pragma unroll
+    for (int k = 0; k < DP; ++k) {
+      y[w][k] = f[k];
+      dy[w][k] = f[DP + k];
+    }
+    hdy[w] = f[2 * DP];
+  }
+
+  // k(x_i, y_j) of one point row (RBF); identical instructions in both sweeps
+  auto krow = [&](const float *__restrict__ xr, float (&k)[W]) {
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      float s = 0.0f;
+#pragma unroll
+      for (int c = 0; c < DP; ++c) {
+        const float t = xr[c] - y[w][c];
+        s = __builtin_fmaf(t, t, s);
+      }
+      k[w] = __builtin_amdgcn_exp2f(s * NHL2E);
+    }
+  };
+  // cells dM(i, j) of row i from k rows i (kc) and i+1 (kn); kcR/knR = right neighbour of column W-1
+  auto cells = [&](const float *__restrict__ fr, const float (&kc)[W], const float (&kn)[W], float kcR, float knR,
+                   float (&dM)[W]) {
+    if constexpr (RBF) {
+      const float hdx = fr[2 * DP];
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        float pp = -hdx, q = -hdy[w], c = 0.0f;
+#pragma unroll
+        for (int k = 0; k < DP; ++k) {
+          const float df = fr[k] - y[w][k];
+          const float dxk = fr[DP + k];
+          pp = __builtin_fmaf(-df, dxk, pp);
+          q = __builtin_fmaf(df, dy[w][k], q);
+          c = __builtin_fmaf(dxk, dy[w][k], c);
+        }
+        const float kn1 = (w + 1 < W) ? kn[w + 1] : knR;
+        const float kc1 = (w + 1 < W) ? kc[w + 1] : kcR;
+        const float naive = (kn1 - kn[w]) - (kc1 - kc[w]);
+        const float Ep = em1_small(pp), Eq = em1_small(q), Ec = em1_small(c);
+        const float stable = kc[w] * __builtin_fmaf(Ep, Eq, (1.0f + Ep) * (1.0f + Eq) * Ec);
+        const float mx = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(pp), __builtin_fabsf(q)), __builtin_fabsf(c));
+        const float v = mx < EM1_TAU ? stable : naive;
+        dM[w] = colv[w] ? v : 0.0f;
+      }
+    } else {
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        float c = 0.0f;
+#pragma unroll
+        for (int k = 0; k < DP; ++k) c = __builtin_fmaf(fr[DP + k], dy[w][k], c);
+        dM[w] = colv[w] ? c : 0.0f;
+      }
+    }
+  };
+
+  // ---- forward sweep
+  float C[M][W];
+#pragma unroll
+  for (int m = 0; m < M; ++m)
+#pragma unroll
+    for (int w = 0; w < W; ++w) C[m][w] = 0.0f;
+  float kc[W], kcR = 0.0f;
+  if constexpr (RBF) {
+    krow(fx, kc);
+    kcR = lane_next(kc[0]);
+  }
+  const int nrows = l1 - 1;
+  for (int i = 0; i < nrows; ++i) {
+    const float *__restrict__ fr = fx + (long long)i * FS;
+    float kn[W], knR = 0.0f, dM[W];
+    if constexpr (RBF) {
+      krow(fr + FS, kn);
+      knR = lane_next(kn[0]);
+    }
+    cells(fr, kc, kn, kcR, knR, dM);
+    if constexpr (M > 1) {
+      float Cs[ML][W], S[ML][W];
+#pragma unroll
+      for (int m = 0; m < ML; ++m)
+#pragma unroll
+        for (int w = 0; w < W; ++w) Cs[m][w] = C[m][w];
+      group_excl_cols_n<LP, W, ML>(Cs, S);
+#pragma unroll
+      for (int m = 1; m < M; ++m)
+#pragma unroll
+        for (int w = 0; w < W; ++w) C[m][w] = __builtin_fmaf(dM[w], S[m - 1][w], C[m][w]);
+    }
+#pragma unroll
+    for (int w = 0; w < W; ++w) C[0][w] += dM[w];
+    if constexpr (RBF) {
+#pragma unroll
+      for (int w = 0; w < W; ++w) kc[w] = kn[w];
+      kcR = knR;
+    }
+  }
+
+  // ---- per-level weights g_m = dLoss/dK_m(a, b) and the normalisation / scale terms
+  float K[M + 1];
+  K[0] = 1.0f;
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    float s = 0.0f;
+#pragma unroll
+    for (int w = 0; w < W; ++w) s += C[m][w];
+    K[m + 1] = group_sum<LP>(s);
+  }
+  K[1] = level1_closed<DP, SEED>(fx, fy, l1, l2);
+
+  float gw[M + 1];
+  {
+    const bool upper_off = p.pair_mode == GPSIG_PAIRS_UPPER && a != bl;
+    const float jit = (p.pair_mode == GPSIG_PAIRS_UPPER && a == bl) ? p.jitter : 0.0f;
+    float gsum = 0.0f;
+    if (!diag && !p.gout_levels) {
+      gsum = p.gout[(long long)a * p.g_ld + bl];
+      if (upper_off) gsum += p.gout[(long long)bl * p.g_ld + a];
+    }
+    float gsc[M + 1];
+#pragma unroll
+    for (int m = 0; m <= M; ++m) {
+      float gs;
+      if (diag) {
+        gs = p.gout[(long long)m * p.g_lvl + a];
+      } else if (p.gout_levels) {
+        gs = p.gout[(long long)m * p.g_lvl + (long long)a * p.g_ld + bl];
+        if (upper_off) gs += p.gout[(long long)m * p.g_lvl + (long long)bl * p.g_ld + a];
+      } else {
+        gs = gsum;
+      }
+      if (!pair_ok) gs = 0.0f;
+      const float sc = p.scale ? p.scale[m] : 1.0f;
+      const float r1 = p.rs1 ? p.rs1[(long long)m * p.n1 + a] : 1.0f;
+      const float r2 = p.rs2 ? p.rs2[(long long)m * p.n2 + bl] : 1.0f;
+      gw[m] = gs * sc * r1 * r2;
+      gsc[m] = gs * (K[m] + jit) * r1 * r2;  // dLoss/dscale_m contribution
+      if (p.rs1 && gl == 0 && pair_ok && !diag) {
+        const float t = gs * sc * (K[m] + jit);
+        if (p.grs1) unsafeAtomicAdd(p.grs1 + (long long)m * p.n1 + a, t * r2);
+        if (p.grs2) unsafeAtomicAdd(p.grs2 + (long long)m * p.n2 + bl, t * r1);
+      }
+    }
+    if (p.gscale && !diag) {
+      // one pair per lane group: keep the group leader's value, then reduce over the wave
+#pragma unroll
+      for (int m = 0; m <= M; ++m) gsc[m] = (gl == 0) ? gsc[m] : 0.0f;
+      wave_sum_last_n<M + 1>(gsc);
+      if (lane == 63)
+        for (int m = 0; m <= M; ++m) unsafeAtomicAdd(p.gscale + m, gsc[m]);
+    }
+  }
+
+  // ---- reverse sweep
+  float Ch[ML][W];
+#pragma unroll
+  for (int m = 0; m < ML; ++m)
+#pragma unroll
+    for (int w = 0; w < W; ++w) Ch[m][w] = gw[m + 1];
+  const float gM = gw[M];
+  float Ep[W], A[W], B[W][DP];
+#pragma unroll
+  for (int w = 0; w < W; ++w) {
+    Ep[w] = 0.0f;
+    A[w] = 0.0f;
+#pragma unroll
+    for (int k = 0; k < DP; ++k) B[w][k] = 0.0f;
+  }
+  float *__restrict__ gxa = p.gX + (long long)a * l1 * p.d;
+  const int d = p.d;
+
+  // point row `pi` of the grid receives dLoss/dk(x_pi, y_j) = Kh[w]: x-gradient reduced over the wave
+  // (all pairs of a wave share a), y-gradient accumulated per column
+  auto emit = [&](int pi, const float (&Kh)[W], const float (&kr)[W]) {
+    const float *__restrict__ xp = fx + (long long)pi * FS;
+    float xi[DP];
+#pragma unroll
+    for (int k = 0; k < DP; ++k) xi[k] = xp[k];
+    float wg[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      const float v = RBF ? Kh[w] * kr[w] : Kh[w];
+      wg[w] = ptv[w] ? v : 0.0f;
+    }
+    float s[DP + 1];
+#pragma unroll
+    for (int k = 0; k <= DP; ++k) s[k] = 0.0f;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      s[DP] += wg[w];
+#pragma unroll
+      for (int k = 0; k < DP; ++k) s[k] = __builtin_fmaf(wg[w], y[w][k], s[k]);
+      A[w] += wg[w];
+#pragma unroll
+      for (int k = 0; k < DP; ++k) B[w][k] = __builtin_fmaf(wg[w], xi[k], B[w][k]);
+    }
+    wave_sum_last_n<DP + 1>(s);
+    if (lane == 63) {
+      for (int k = 0; k < d; ++k) {
+        const float v = RBF ? __builtin_fmaf(-s[DP], xi[k], s[k]) : s[k];
+        unsafeAtomicAdd(gxa + (long long)pi * d + k, v);
+      }
+    }
+  };
+
+  float kr1[W], kr1R = 0.0f;  // k row i+1
+  if constexpr (RBF) {
+#pragma unroll
+    for (int w = 0; w < W; ++w) kr1[w] = kc[w];
+    kr1R = kcR;
+  } else {
+#pragma unroll
+    for (int w = 0; w < W; ++w) kr1[w] = 1.0f;
+  }
+  for (int i = nrows - 1; i >= 0; --i) {
+    const float *__restrict__ fr = fx + (long long)i * FS;
+    float k0[W], k0R = 0.0f, dM[W];
+    if constexpr (RBF) {
+      krow(fr, k0);
+      k0R = lane_next(k0[0]);
+    } else {
+#pragma unroll
+      for (int w = 0; w < W; ++w) k0[w] = 1.0f;
+    }
+    cells(fr, k0, kr1, k0R, kr1R, dM);
+
+    // forward state of row i: C_m(i) = C_m(i+1) - dM S_{m-1}(i), ascending levels (C[m] holds level m+1,
+    // S_0 = 1), and dLoss/d dM(i, j) = sum_m Ch_m(i+1, j) S_{m-1}(i, j)
+    float Dh[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      C[0][w] -= dM[w];
+      Dh[w] = (M > 1) ? Ch[0][w] : gM;
+    }
+#pragma unroll
+    for (int s = 1; s < M; ++s) {
+      float Cm[1][W], Sm[1][W];
+#pragma unroll
+      for (int w = 0; w < W; ++w) Cm[0][w] = C[s - 1][w];
+      group_excl_cols_n<LP, W, 1>(Cm, Sm);  // S_s(i) from the recovered C_s(i)
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        if (s + 1 < M) C[s][w] = __builtin_fmaf(-dM[w], Sm[0][w], C[s][w]);
+        const float chn = (s + 1 < M) ? Ch[s < ML ? s : 0][w] : gM;  // Ch_{s+1}
+        Dh[w] = __builtin_fmaf(chn, Sm[0][w], Dh[w]);
+      }
+    }
+#pragma unroll
+    for (int w = 0; w < W; ++w) Dh[w] = colv[w] ? Dh[w] : 0.0f;
+
+    // adjoint column sums: Ch_m(i) = Ch_m(i+1) + rexcl(dM * Ch_{m+1}(i+1)), ascending m (old Ch_{m+1})
+    if constexpr (M > 1) {
+      float v[ML][W], r[ML][W];
+#pragma unroll
+      for (int m = 0; m < ML; ++m)
+#pragma unroll
+        for (int w = 0; w < W; ++w) v[m][w] = dM[w] * ((m + 1 < ML) ? Ch[m + 1][w] : gM);
+      group_rexcl_cols_n<LP, W, ML>(v, r);
+#pragma unroll
+      for (int m = 0; m < ML; ++m)
+#pragma unroll
+        for (int w = 0; w < W; ++w) Ch[m][w] += r[m][w];
+    }
+
+    // adjoint of the second difference: E(i, j) = Dh(i, j-1) - Dh(i, j); Kh(i+1, j) = E(i, j) - E(i+1, j)
+    float left = lane_prev(Dh[W - 1]);
+    if (gl == 0) left = 0.0f;
+    float Kh[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      const float e = ((w == 0) ? left : Dh[w - 1]) - Dh[w];
+      Kh[w] = e - Ep[w];
+      Ep[w] = e;
+    }
+    emit(i + 1, Kh, kr1);
+#pragma unroll
+    for (int w = 0; w < W; ++w) kr1[w] = k0[w];
+    kr1R = k0R;
+  }
+  {
+    float Kh[W];
+#pragma unroll
+    for (int w = 0; w < W; ++w) Kh[w] = -Ep[w];
+    emit(0, Kh, kr1);
+  }
+
+  // ---- y-gradient of the pair's columns
+  if (pair_ok) {
+    float *__restrict__ gyb = (diag ? p.gX : p.gY) + (long long)bl * l2 * d;
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      const int j = gl * W + w;
+      if (!ptv[w]) continue;
+      for (int k = 0; k < d; ++k) {
+        const float v = RBF ? __builtin_fmaf(-A[w], y[w][k], B[w][k]) : B[w][k];
+        unsafeAtomicAdd(gyb + (long long)j * d + k, v);
+      }
+    }
+  }
+}
+
+// Column geometry of the backward kernel: W columns per lane, LP lanes per pair.  The lane keeps
+// y, dy and the y-gradient accumulator (3 W DP floats) plus 2 (M-1) W level states.
+struct BwdGeo { int W, LP; };
+inline BwdGeo bwd_geometry(int l2, int DP) {
+  const int W = DP <= 8 ? 4 : 2;
+  for (int LP : {16, 32, 64})
+    if (LP * W >= l2) return {W, LP};
+  return {0, 0};
+}
+
+}  // namespace gpsig

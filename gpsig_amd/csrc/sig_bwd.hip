@@ -1,0 +1,118 @@
+// gpsig_amd -- extern "C" entry of the first-order Gram VJP (include/gpsig_amd.h, gpsig_sig_gram_vjp):
+// argument checks, feature records, tile counts, dispatch to the per-(DP, M) instantiations of
+// sig_bwd_kernel (sig_bwd.h, sig_bwd_inst.hip).
+#include "sig_bwd.h"
+
+namespace gpsig {
+int features(const float *X, int n, int l, int d, int DP, float *F, hipStream_t s);
+template <int DP, int M>
+int sig_bwd_launch_dpm(const BwdArgs &a, int seed, long long nblocks, hipStream_t s);
+
+template <int DP>
+static int bwd_dp(const BwdArgs &a, int seed, long long nblocks, hipStream_t s) {
+  switch (a.M) {
+    case 1: return sig_bwd_launch_dpm<DP, 1>(a, seed, nblocks, s);
+    case 2: return sig_bwd_launch_dpm<DP, 2>(a, seed, nblocks, s);
+    case 3: return sig_bwd_launch_dpm<DP, 3>(a, seed, nblocks, s);
+    case 4: return sig_bwd_launch_dpm<DP, 4>(a, seed, nblocks, s);
+    case 5: return sig_bwd_launch_dpm<DP, 5>(a, seed, nblocks, s);
+    case 6: return sig_bwd_launch_dpm<DP, 6>(a, seed, nblocks, s);
+    case 7: return sig_bwd_launch_dpm<DP, 7>(a, seed, nblocks, s);
+    case 8: return sig_bwd_launch_dpm<DP, 8>(a, seed, nblocks, s);
+    default: return GPSIG_EUNSUPPORTED;
+  }
+}
+
+// channel padding of the VJP instantiations (never wider than the forward's workspace padding)
+static int bwd_pad(int d) {
+  if (d <= 6) return d;
+  if (d <= 8) return 8;
+  if (d <= 16) return 16;
+  return 0;
+}
+
+static size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
+static inline long long upper_prefix(long long r, long long ntb, long long k) { return r * ntb - k * r * (r - 1) / 2; }
+
+}  // namespace gpsig
+
+using namespace gpsig;
+
+extern "C" int gpsig_sig_gram_vjp(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d,
+                                  int num_levels, int base_kind, int pair_mode, int row_begin, int row_end,
+                                  const float *gout, int gout_levels, const float *rs1, const float *rs2,
+                                  const float *scale, float jitter, float *gX, float *gY, float *grs1, float *grs2,
+                                  float *gscale, void *workspace, size_t workspace_bytes, gpsig_stream_t stream) {
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (!X || !Y || !gout || !gX || n1 <= 0 || n2 <= 0 || d <= 0 || num_levels < 1) return GPSIG_EINVAL;
+  if (l1 < 2 || l2 < 2) return GPSIG_EINVAL;
+  if (pair_mode < GPSIG_PAIRS_RECT || pair_mode > GPSIG_PAIRS_DIAG) return GPSIG_EINVAL;
+  if (row_begin < 0 || row_end > n1 || row_begin > row_end) return GPSIG_EINVAL;
+  if (pair_mode != GPSIG_PAIRS_RECT && (n1 != n2 || l1 != l2 || X != Y)) return GPSIG_EINVAL;
+  if (pair_mode == GPSIG_PAIRS_RECT && !gY) return GPSIG_EINVAL;
+  if (pair_mode == GPSIG_PAIRS_DIAG && !gout_levels) return GPSIG_EINVAL;
+  if ((rs1 == nullptr) != (rs2 == nullptr)) return GPSIG_EINVAL;
+  const int seed = base_kind == GPSIG_BASE_RBF ? SEED_RBF_DIFF : (base_kind == GPSIG_BASE_LINEAR ? SEED_LIN_DIFF : -1);
+  const int DP = bwd_pad(d);
+  if (seed < 0 || DP == 0) return GPSIG_EUNSUPPORTED;
+  const BwdGeo geo = bwd_geometry(l2, DP);
+  if (geo.W == 0 || num_levels > 8) return GPSIG_EUNSUPPORTED;
+  if (row_end == row_begin) return GPSIG_OK;
+
+  const bool same = (X == Y && n1 == n2 && l1 == l2);
+  const size_t fx_b = align256((size_t)n1 * l1 * feat_stride(DP) * sizeof(float));
+  const size_t fy_b = same ? 0 : align256((size_t)n2 * l2 * feat_stride(DP) * sizeof(float));
+  if (!workspace || workspace_bytes < fx_b + fy_b) return GPSIG_EWORKSPACE;
+  float *FX = static_cast<float *>(workspace);
+  float *FY = same ? FX : reinterpret_cast<float *>(static_cast<char *>(workspace) + fx_b);
+  int rc = features(X, n1, l1, d, DP, FX, s);
+  if (rc) return rc;
+  if (!same && (rc = features(Y, n2, l2, d, DP, FY, s))) return rc;
+
+  BwdArgs a{};
+  a.FX = FX;
+  a.FY = FY;
+  a.n1 = n1; a.l1 = l1; a.n2 = n2; a.l2 = l2; a.d = d;
+  a.M = num_levels;
+  a.pair_mode = pair_mode;
+  a.row_begin = row_begin;
+  a.row_end = row_end;
+  a.gout = gout;
+  a.gout_levels = gout_levels ? 1 : 0;
+  a.g_ld = n2;
+  a.g_lvl = pair_mode == GPSIG_PAIRS_DIAG ? (long long)n1 : (long long)n1 * n2;
+  a.rs1 = rs1; a.rs2 = rs2; a.scale = scale;
+  a.jitter = jitter;
+  a.gX = gX;
+  a.gY = pair_mode == GPSIG_PAIRS_RECT ? gY : gX;
+  a.grs1 = grs1;
+  a.grs2 = pair_mode == GPSIG_PAIRS_RECT ? grs2 : grs1;
+  a.gscale = gscale;
+
+  const int G = 64 / geo.LP;
+  long long nblocks;
+  if (pair_mode == GPSIG_PAIRS_DIAG) {
+    nblocks = (row_end - row_begin + 3) / 4;
+  } else {
+    const int ta0 = row_begin / 4, ta1 = (row_end + 3) / 4;
+    const int ntb = (n2 + G - 1) / G;
+    a.tiles_a0 = ta0;
+    a.ntb = ntb;
+    if (pair_mode == GPSIG_PAIRS_RECT) {
+      nblocks = (long long)(ta1 - ta0) * ntb;
+    } else {
+      const int k = 4 / G;
+      a.tile_base = upper_prefix(ta0, ntb, k);
+      nblocks = upper_prefix(ta1, ntb, k) - a.tile_base;
+    }
+  }
+  if (nblocks > 0x7fffffffLL) return GPSIG_EUNSUPPORTED;
+  if (nblocks <= 0) return GPSIG_OK;
+  switch (DP) {
+#define CASE(v) \
+  case v: return bwd_dp<v>(a, seed, nblocks, s);
+    CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(8) CASE(16)
+#undef CASE
+    default: return GPSIG_EUNSUPPORTED;
+  }
+}

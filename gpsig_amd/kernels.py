@@ -17,6 +17,7 @@ import numpy as np
 import torch
 
 from . import _lib as L
+from . import autograd as _ag
 from . import lags as _lags
 from . import ops
 
@@ -160,9 +161,13 @@ class SignatureKernel:
         return X.dtype if (isinstance(X, torch.Tensor) and X.is_floating_point()) else torch.float64
 
     # ------------------------------------------------------------------ algorithm seam (kernels.py:190-341)
+    def _cfg(self, return_levels=False):
+        return dict(num_levels=self.num_levels, order=self.order, base=self.base, difference=self.difference,
+                    normalization=self.normalization, jitter=self.jitter, return_levels=bool(return_levels))
+
     def _K_seq_diag(self, X):
-        """(N,L,D) scaled -> (num_levels+1, N) unnormalised diagonal (kernels.py:190-207)."""
-        return ops.sig_diag(X, self.num_levels, self.order, self.base, self.difference)
+        """(N,L,D) scaled -> (num_levels+1, N) unnormalised diagonal (kernels.py:190-207); differentiable."""
+        return _ag.SigDiag.apply(X, self._cfg())
 
     def _K_seq(self, X, X2=None):
         """(N,L,D) scaled -> (num_levels+1, N, N2) unnormalised per-level Gram (kernels.py:209-238)."""
@@ -179,19 +184,10 @@ class SignatureKernel:
             presliced_X = presliced_X2 = True
         dt = self._out_dtype(X)
         Xs = self._prep(X, presliced_X)
-        scale = self._scale_vec(Xs.device)
-        mode = L.OUT_NORM_LEVELS if return_levels else L.OUT_NORM_SUM
-        if X2 is None:
-            rs = self._rsqrt_diag(Xs) if self.normalization else None
-            out = ops.sig_gram(Xs, None, self.num_levels, self.order, self.base, self.difference, rs1=rs, rs2=rs,
-                               scale=scale, jitter=self.jitter if self.normalization else 0.0, out_mode=mode)
-        else:
-            X2s = self._prep(X2, presliced_X2)
-            rs1 = rs2 = None
-            if self.normalization:
-                rs1, rs2 = self._rsqrt_diag(Xs), self._rsqrt_diag(X2s)
-            out = ops.sig_gram(Xs, X2s, self.num_levels, self.order, self.base, self.difference, rs1=rs1, rs2=rs2,
-                               scale=scale, out_mode=mode)
+        X2s = None if X2 is None else self._prep(X2, presliced_X2)
+        scale = (self.sigma * self.variances).to(Xs.device)
+        # forward: fused Gram kernel; backward (autograd): gpsig_sig_gram_vjp (gpsig_amd/autograd.py)
+        out = _ag.SigGram.apply(Xs, X2s, scale, self._cfg(return_levels))
         return out.to(dt)
 
     def K_norms(self, X, presliced=False):
@@ -212,7 +208,7 @@ class SignatureKernel:
                 return sv[:, None].repeat(1, N)
             return torch.full((N,), float(sv.sum()), dtype=dt, device=Xt.device)
         Xs = self._prep(Xt, presliced)
-        Kd = self._K_seq_diag(Xs) * self._scale_vec(Xs.device)[:, None]
+        Kd = self._K_seq_diag(Xs) * (self.sigma * self.variances).to(Xs.device, torch.float32)[:, None]
         return (Kd if return_levels else Kd.sum(0)).to(dt)
 
     # ------------------------------------------------------------------ inducing tensors (kernels.py:544-704)

@@ -114,6 +114,56 @@ def sig_gram(X: torch.Tensor, Y: torch.Tensor | None, num_levels: int, order: in
     return out
 
 
+def sig_gram_vjp(X: torch.Tensor, Y: torch.Tensor | None, num_levels: int, gout: torch.Tensor, base="rbf",
+                 gout_levels: bool = False, diag: bool = False, rs1=None, rs2=None, scale=None, jitter: float = 0.0,
+                 gX: torch.Tensor | None = None, gY: torch.Tensor | None = None, grs1=None, grs2=None,
+                 gscale=None, rows: tuple | None = None):
+    """dLoss/dX (and dLoss/dY, dLoss/drs, dLoss/dscale) of the first-order Gram, accumulated into float32
+    buffers: see gpsig_sig_gram_vjp in include/gpsig_amd.h.  Y None -> symmetric K(X) (or the diagonal
+    with diag=True; gout is then (num_levels+1, n) per level).  Returns (gX, gY)."""
+    _require_cuda(X, Y, gout, rs1, rs2, scale)
+    lib = L.load()
+    X = _f32(X)
+    sym = Y is None
+    Y = X if sym else _f32(Y)
+    n1, l1, d = X.shape
+    n2, l2, d2 = Y.shape
+    if d2 != d:
+        raise ValueError("X and Y must have the same channel count")
+    gout = _f32(gout)
+    if diag:
+        if not sym:
+            raise ValueError("diag=True needs Y=None")
+        if tuple(gout.shape) != (num_levels + 1, n1):
+            raise ValueError(f"diagonal gout must be (num_levels+1, n) = {(num_levels + 1, n1)}")
+        gout_levels = True
+    else:
+        want = (num_levels + 1, n1, n2) if gout_levels else (n1, n2)
+        if tuple(gout.shape) != want:
+            raise ValueError(f"gout must have shape {want}, got {tuple(gout.shape)}")
+    r0, r1 = (0, n1) if rows is None else rows
+    if gX is None:
+        gX = torch.zeros((n1, l1, d), dtype=torch.float32, device=X.device)
+    if not sym and gY is None:
+        gY = torch.zeros((n2, l2, d), dtype=torch.float32, device=X.device)
+    for t, shp in ((gX, (n1, l1, d)), (gY, None if sym else (n2, l2, d))):
+        if shp is not None and (t.dtype != torch.float32 or not t.is_contiguous() or tuple(t.shape) != shp):
+            raise ValueError(f"gradient buffers must be contiguous float32 {shp}")
+    if rs1 is not None:
+        rs1, rs2 = _f32(rs1), _f32(rs2)
+    if scale is not None:
+        scale = _f32(scale)
+    nb = lib.gpsig_sig_workspace_bytes(n1, l1, n2, l2, d)
+    ws = workspace(X.device, nb)
+    mode = L.PAIRS_DIAG if diag else (L.PAIRS_UPPER if sym else L.PAIRS_RECT)
+    rc = lib.gpsig_sig_gram_vjp(X.data_ptr(), n1, l1, Y.data_ptr(), n2, l2, d, num_levels, base_kind(base), mode, r0, r1,
+                                gout.data_ptr(), int(bool(gout_levels)), _ptr(rs1), _ptr(rs2), _ptr(scale),
+                                float(jitter), gX.data_ptr(), _ptr(gY), _ptr(grs1), _ptr(grs2), _ptr(gscale),
+                                ws.data_ptr(), ws.numel(), _stream(X.device))
+    L.check(rc, "gpsig_sig_gram_vjp")
+    return gX, gY
+
+
 # ----------------------------------------------------------------------------- PDE kernel
 def pde_diag(X: torch.Tensor, dyadic: int = 0, solver: int = 1) -> torch.Tensor:
     _require_cuda(X)

@@ -89,6 +89,29 @@ int gpsig_sig_diag(const float *X, int n, int l, int d, int num_levels, int orde
                    gpsig_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
+ * Gradient of the first-order Gram (vector-Jacobian product).
+ *
+ * The reference obtains dLoss/dX of K (and through the host-side scaling dLoss/dlengthscales) by TF
+ * autodiff of the graph kernels.py:209-238 (base kernel, kernels.py:946-1044) ->
+ * signature_algs.py:8-35 -> kernels.py:431-477 (jitter, normalisation, sigma*variances).  This entry
+ * evaluates the same derivative for order == 1 and difference == True (RBF and linear seeds):
+ *
+ *   gout_levels == 0: gout (n1, n2) is dLoss/dK for out_mode GPSIG_OUT_NORM_SUM;
+ *   gout_levels == 1: gout (L+1, n1, n2) is dLoss/dK_m for GPSIG_OUT_LEVELS / GPSIG_OUT_NORM_LEVELS;
+ *   GPSIG_PAIRS_DIAG: gout (L+1, n1) per-level dLoss/dK_m(a, a) of gpsig_sig_diag (gout_levels = 1).
+ *   rs1/rs2/scale/jitter: as in the forward call (NULL = none).  Accumulated (+=) outputs:
+ *   gX (n1, l1, d) and gY (n2, l2, d) (UPPER / DIAG: Y == X and everything goes to gX);
+ *   grs1 (L+1, n1), grs2 (L+1, n2) = dLoss/drs (the host chains them through rs = (diag+jitter)^-1/2
+ *   into a DIAG call); gscale (L+1) = dLoss/dscale.  Any of grs1/grs2/gscale may be NULL.
+ *   Workspace: gpsig_sig_workspace_bytes(n1, l1, n2, l2, d).
+ */
+int gpsig_sig_gram_vjp(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int num_levels,
+                       int base_kind, int pair_mode, int row_begin, int row_end, const float *gout, int gout_levels,
+                       const float *rs1, const float *rs2, const float *scale, float jitter, float *gX, float *gY,
+                       float *grs1, float *grs2, float *gscale, void *workspace, size_t workspace_bytes,
+                       gpsig_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------
  * Inducing tensors (sparse rank-1 tensors z = (z_{m,1} (x) ... (x) z_{m,m})_m).
  *
  * gpsig_tens_vs_seq replaces _K_tens_vs_seq (kernels.py:314-341) = base kernel between tensor

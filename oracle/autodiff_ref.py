@@ -1,0 +1,95 @@
+"""CPU oracle for GRADIENTS: float64 torch restatement of the reference graph, differentiated by
+torch.autograd the way the reference is differentiated by TF autodiff.
+
+TEST INFRASTRUCTURE ONLY (see oracle/sigalgs.py header): only tests/ may import it, as the checker
+of gpsig_sig_gram_vjp / gpsig_amd.autograd.
+
+The reference has no hand-written gradient for the truncated signature kernel: SVGP training
+differentiates K through TF-1.15 autodiff of the graph (file:line relative to /root/reference)
+
+  * base kernels                 gpsig/kernels.py:946-957 (_square_dist), :979-986 (_lin), :1042-1044 (_rbf)
+  * second difference + recursion gpsig/signature_algs.py:8-35 (signature_kern_first_order)
+  * scaling                      gpsig/kernels.py:344-365 (X / lengthscales; num_lags=0)
+  * K: jitter, normalisation by sqrt(diag), sigma*variances, level sum   gpsig/kernels.py:402-477
+  * Kdiag (unnormalised)         gpsig/kernels.py:510-541
+
+restated here op for op on torch float64 tensors (materialised base-kernel tensor, exclusive cumsums
+as shifted cumsums, diag of the Gram for K(X)).  Reverse-mode autodiff of the same function in fp64
+is the reference's gradient up to fp64 rounding.  Pinning: the forward values equal oracle/sigalgs.py
+/ oracle/kernels_ref.py (the pinned NumPy restatement) and the gradients equal central finite
+differences of that NumPy oracle (tests/test_oracle.py).
+"""
+from __future__ import annotations
+
+import torch
+
+
+def _xcumsum(a: torch.Tensor, dim: int) -> torch.Tensor:
+    """tf.cumsum(a, exclusive=True, axis=dim)."""
+    c = torch.cumsum(a, dim)
+    z = torch.zeros_like(c.narrow(dim, 0, 1))
+    return torch.cat([z, c.narrow(dim, 0, c.shape[dim] - 1)], dim)
+
+
+def square_dist(X, X2):
+    """kernels.py:946-957: |x|^2 + |y|^2 - 2 x.y."""
+    Xs = (X ** 2).sum(-1)
+    X2s = (X2 ** 2).sum(-1)
+    return -2.0 * X @ X2.T + Xs[:, None] + X2s[None, :]
+
+
+def base_kern(X, X2, base):
+    if base == "rbf":
+        return torch.exp(-square_dist(X, X2) / 2.0)  # kernels.py:1042-1044
+    return X @ X2.T  # kernels.py:979-986
+
+
+def first_order(M: torch.Tensor, num_levels: int, difference: bool = True) -> torch.Tensor:
+    """signature_algs.py:8-35 on a 4-D (n1, l1, n2, l2) tensor -> (num_levels+1, n1, n2)."""
+    K = [torch.ones((M.shape[0], M.shape[2]), dtype=M.dtype)]
+    if difference:
+        M = M[:, 1:, :, 1:] + M[:, :-1, :, :-1] - M[:, :-1, :, 1:] - M[:, 1:, :, :-1]
+    K.append(M.sum(dim=(1, -1)))
+    R = M
+    for _ in range(2, num_levels + 1):
+        R = M * _xcumsum(_xcumsum(R, 1), -1)
+        K.append(R.sum(dim=(1, -1)))
+    return torch.stack(K, 0)
+
+
+def k_seq(Xs, X2s, num_levels, base="rbf", difference=True):
+    """_K_seq (kernels.py:209-238) for order 1: Xs (n1,l1,d), X2s (n2,l2,d) or None."""
+    n1, l1, d = Xs.shape
+    Y = Xs if X2s is None else X2s
+    n2, l2, _ = Y.shape
+    M = base_kern(Xs.reshape(n1 * l1, d), Y.reshape(n2 * l2, d), base).reshape(n1, l1, n2, l2)
+    return first_order(M, num_levels, difference)
+
+
+def k_seq_diag(Xs, num_levels, base="rbf", difference=True):
+    """_K_seq_diag (kernels.py:190-207): per-sequence (n, l, l) base kernel -> (num_levels+1, n)."""
+    n, l, d = Xs.shape
+    Ms = torch.stack([base_kern(Xs[a], Xs[a], base) for a in range(n)], 0)  # (n, l, l)
+    M = Ms[:, :, None, :]  # run the 3-D branch as a (n, l, 1, l) tensor
+    K = first_order(M, num_levels, difference)  # (M+1, n, 1)
+    return K[:, :, 0]
+
+
+def K(Xs, X2s, num_levels, base="rbf", normalization=True, scale=None, jitter=1e-6, return_levels=False,
+      difference=True):
+    """SignatureKernel.K (kernels.py:402-477) on scaled sequences; scale = sigma * variances (M+1)."""
+    K_l = k_seq(Xs, X2s, num_levels, base, difference)
+    if normalization:
+        if X2s is None:
+            n = Xs.shape[0]
+            K_l = K_l + jitter * torch.eye(n, dtype=K_l.dtype)[None]
+            dsq = torch.sqrt(torch.diagonal(K_l, dim1=1, dim2=2))
+            K_l = K_l / (dsq[:, :, None] * dsq[:, None, :])
+        else:
+            d1 = torch.sqrt(k_seq_diag(Xs, num_levels, base, difference) + jitter)
+            d2 = torch.sqrt(k_seq_diag(X2s, num_levels, base, difference) + jitter)
+            K_l = K_l / (d1[:, :, None] * d2[:, None, :])
+    if scale is None:
+        scale = torch.ones(num_levels + 1, dtype=K_l.dtype)
+    K_l = K_l * scale[:, None, None]
+    return K_l if return_levels else K_l.sum(0)

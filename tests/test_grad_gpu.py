@@ -1,0 +1,148 @@
+"""GPU parity of the gradients: gpsig_sig_gram_vjp (through gpsig_amd.autograd) vs torch fp64 autodiff
+of the reference graph (oracle/autodiff_ref.py, pinned by finite differences in test_grad_oracle.py).
+
+Criterion: norm-relative max|g32 - g64| <= GTOL * max|g64| per gradient tensor.  The forward is fp32
+(1e-5 bar); a gradient chains one more fp32 sweep, so the bar is 5e-5.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import norm_rel_err
+from oracle import autodiff_ref as ar
+
+pytestmark = pytest.mark.gpu
+GTOL = 5e-5
+DEV = "cuda"
+
+
+def walks(n, l, d, seed, scale=1.0):
+    rng = np.random.default_rng(seed)
+    return scale * np.cumsum(rng.standard_normal((n, l, d)), axis=1) / np.sqrt(l * d)
+
+
+def grads_gpu(kern, X, X2, G, return_levels=False, params=()):
+    Xt = torch.tensor(X.reshape(len(X), -1), device=DEV, requires_grad=True)
+    X2t = None if X2 is None else torch.tensor(X2.reshape(len(X2), -1), device=DEV, requires_grad=True)
+    K = kern.K(Xt, X2t, return_levels=return_levels)
+    (K * torch.as_tensor(G, device=DEV)).sum().backward()
+    out = [Xt.grad.reshape(X.shape).cpu().numpy()]
+    if X2 is not None:
+        out.append(X2t.grad.reshape(X2.shape).cpu().numpy())
+    out += [p.grad.cpu().numpy() for p in params]
+    return out, K.detach().cpu().numpy()
+
+
+def grads_ref(X, X2, G, M, base="rbf", normalization=True, return_levels=False, lengthscales=None, variances=None,
+              jitter=1e-6):
+    Xt = torch.tensor(X, requires_grad=True)
+    X2t = None if X2 is None else torch.tensor(X2, requires_grad=True)
+    ls = torch.tensor(np.ones(X.shape[-1]) if lengthscales is None else lengthscales, requires_grad=True)
+    var = torch.tensor(np.ones(M + 1) if variances is None else variances, requires_grad=True)
+    K = ar.K(Xt / ls, None if X2t is None else X2t / ls, M, base=base, normalization=normalization, scale=var,
+             jitter=jitter, return_levels=return_levels)
+    (K * torch.tensor(G)).sum().backward()
+    out = [Xt.grad.numpy()]
+    if X2 is not None:
+        out.append(X2t.grad.numpy())
+    return out, ls.grad.numpy(), var.grad.numpy(), K.detach().numpy()
+
+
+@pytest.mark.parametrize("base", ["rbf", "linear"])
+@pytest.mark.parametrize("cross", [False, True])
+@pytest.mark.parametrize("normalization", [True, False])
+def test_gram_vjp_matches_autodiff(base, cross, normalization):
+    import gpsig_amd
+    N, N2, L, L2, D, M = 12, 9, 24, 17, 3, 4
+    X = walks(N, L, D, 0)
+    X2 = walks(N2, L2, D, 1) if cross else None
+    if cross:
+        X2 = walks(N2, L, D, 1)  # the API takes one length per kernel (input_dim = L*D)
+    G = np.random.default_rng(2).standard_normal((N, N2 if cross else N))
+    cls = gpsig_amd.SignatureRBF if base == "rbf" else gpsig_amd.SignatureLinear
+    k = cls(L * D, D, M, normalization=normalization)
+    got, K = grads_gpu(k, X, X2, G)
+    ref, _, _, Kref = grads_ref(X, X2, G, M, base=base, normalization=normalization)
+    assert norm_rel_err(K, Kref) < 1e-5
+    for g, r in zip(got, ref):
+        assert norm_rel_err(g, r) < GTOL, (norm_rel_err(g, r))
+
+
+def test_gram_vjp_return_levels_lengthscales_variances():
+    import gpsig_amd
+    N, L, D, M = 10, 20, 2, 5
+    X = walks(N, L, D, 3)
+    G = np.random.default_rng(4).standard_normal((M + 1, N, N))
+    ls = np.array([0.7, 1.3])
+    var = np.array([0.5, 1.0, 2.0, 1.5, 0.8, 1.2])
+    k = gpsig_amd.SignatureRBF(L * D, D, M, lengthscales=ls, variances=var)
+    k.lengthscales = torch.tensor(ls, device=DEV, requires_grad=True)
+    k.variances = torch.tensor(var, device=DEV, requires_grad=True)
+    got, K = grads_gpu(k, X, None, G, return_levels=True, params=(k.lengthscales, k.variances))
+    ref, gls, gvar, Kref = grads_ref(X, None, G, M, return_levels=True, lengthscales=ls, variances=var)
+    assert norm_rel_err(K, Kref) < 1e-5
+    assert norm_rel_err(got[0], ref[0]) < GTOL
+    assert norm_rel_err(got[1], gls) < GTOL
+    assert norm_rel_err(got[2], gvar) < GTOL
+
+
+@pytest.mark.parametrize("D,M,L", [(1, 1, 8), (5, 8, 40), (8, 2, 33), (16, 3, 20), (5, 5, 128)])
+def test_gram_vjp_shapes(D, M, L):
+    import gpsig_amd
+    N = 6 if L > 64 else 9
+    X = walks(N, L, D, 5)
+    G = np.random.default_rng(6).standard_normal((N, N))
+    k = gpsig_amd.SignatureRBF(L * D, D, M)
+    got, _ = grads_gpu(k, X, None, G)
+    ref, _, _, _ = grads_ref(X, None, G, M)
+    assert norm_rel_err(got[0], ref[0]) < GTOL
+
+
+def test_kdiag_unnormalised_vjp():
+    import gpsig_amd
+    N, L, D, M = 7, 30, 3, 4
+    X = walks(N, L, D, 7, scale=2.0)
+    k = gpsig_amd.SignatureRBF(L * D, D, M, normalization=False)
+    Xt = torch.tensor(X.reshape(N, -1), device=DEV, requires_grad=True)
+    w = np.random.default_rng(8).standard_normal((M + 1, N))
+    (k.Kdiag(Xt, return_levels=True) * torch.as_tensor(w, device=DEV)).sum().backward()
+    Xr = torch.tensor(X, requires_grad=True)
+    (ar.k_seq_diag(Xr, M) * torch.tensor(w)).sum().backward()
+    assert norm_rel_err(Xt.grad.reshape(X.shape).cpu().numpy(), Xr.grad.numpy()) < GTOL
+
+
+def test_rough_data_vjp():
+    """Large increments (|p|, |c| beyond the polynomial range): the corner-difference cells."""
+    import gpsig_amd
+    rng = np.random.default_rng(9)
+    N, L, D, M = 6, 16, 3, 3
+    X = rng.standard_normal((N, L, D))
+    G = rng.standard_normal((N, N))
+    k = gpsig_amd.SignatureRBF(L * D, D, M)
+    got, _ = grads_gpu(k, X, None, G)
+    ref, _, _, _ = grads_ref(X, None, G, M)
+    assert norm_rel_err(got[0], ref[0]) < GTOL
+
+
+def test_higher_order_backward_raises():
+    import gpsig_amd
+    X = walks(4, 10, 2, 0)
+    k = gpsig_amd.SignatureRBF(20, 2, 3, order=2)
+    Xt = torch.tensor(X.reshape(4, -1), device=DEV, requires_grad=True)
+    with pytest.raises(NotImplementedError):
+        k.K(Xt).sum().backward()
+
+
+@pytest.mark.parametrize("base", ["rbf", "linear"])
+def test_raw_levels_vjp_ragged_lengths(base):
+    """ops-level VJP of the raw per-level Gram with l1 != l2 (padded lane columns on both sides)."""
+    from gpsig_amd import ops
+    N1, N2, L1, L2, D, M = 5, 7, 19, 45, 4, 6
+    X, Y = walks(N1, L1, D, 10), walks(N2, L2, D, 11)
+    G = np.random.default_rng(12).standard_normal((M + 1, N1, N2))
+    gX, gY = ops.sig_gram_vjp(torch.tensor(X, device=DEV), torch.tensor(Y, device=DEV), M,
+                              torch.tensor(G, device=DEV), base=base, gout_levels=True)
+    Xr, Yr = torch.tensor(X, requires_grad=True), torch.tensor(Y, requires_grad=True)
+    (ar.k_seq(Xr, Yr, M, base) * torch.tensor(G)).sum().backward()
+    assert norm_rel_err(gX.cpu().numpy(), Xr.grad.numpy()) < GTOL
+    assert norm_rel_err(gY.cpu().numpy(), Yr.grad.numpy()) < GTOL

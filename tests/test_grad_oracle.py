@@ -1,0 +1,61 @@
+"""CPU: pin the gradient oracle (oracle/autodiff_ref.py, torch fp64 autodiff of the reference graph).
+
+Forward values must equal the pinned NumPy oracle (oracle/kernels_ref.py); gradients must equal
+central finite differences of that NumPy oracle -- i.e. the derivative TF autodiff computes for the
+reference graph (gpsig/kernels.py:402-477 over signature_algs.py:8-35).
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import autodiff_ref as ar
+from oracle import kernels_ref as kr
+
+
+def walks(n, l, d, seed):
+    rng = np.random.default_rng(seed)
+    return np.cumsum(rng.standard_normal((n, l, d)), axis=1) / np.sqrt(l * d)
+
+
+@pytest.mark.parametrize("base", ["rbf", "linear"])
+@pytest.mark.parametrize("cross", [False, True])
+def test_autodiff_oracle_forward_matches_numpy_oracle(base, cross):
+    X, X2 = walks(5, 7, 2, 0), walks(4, 9, 2, 1)
+    M = 3
+    k = kr.SignatureKernelRef(7 * 2, 2, M, base=base)
+    ref = k.K(X.reshape(5, -1), None if not cross else X2.reshape(4, -1), return_levels=True) if not cross else None
+    if cross:
+        k2 = kr.SignatureKernelRef(7 * 2, 2, M, base=base)
+        # the NumPy oracle takes sequences of one length per call; cross lengths differ here
+        ref = k2.K(X.reshape(5, -1), X2[:, :7].reshape(4, -1), return_levels=True)
+        got = ar.K(torch.tensor(X), torch.tensor(X2[:, :7]), M, base=base, return_levels=True).numpy()
+    else:
+        got = ar.K(torch.tensor(X), None, M, base=base, return_levels=True).numpy()
+    np.testing.assert_allclose(got, ref, rtol=1e-11, atol=1e-13)
+
+
+@pytest.mark.parametrize("base", ["rbf", "linear"])
+def test_autodiff_oracle_gradient_matches_finite_differences(base):
+    X, X2 = walks(3, 6, 2, 3), walks(2, 6, 2, 4)
+    M = 3
+    rng = np.random.default_rng(5)
+    G = rng.standard_normal((3, 2))
+    k = kr.SignatureKernelRef(6 * 2, 2, M, base=base)
+
+    def loss(Xv, X2v):
+        return float((k.K(Xv.reshape(3, -1), X2v.reshape(2, -1)) * G).sum())
+
+    Xt = torch.tensor(X, requires_grad=True)
+    X2t = torch.tensor(X2, requires_grad=True)
+    (ar.K(Xt, X2t, M, base=base) * torch.tensor(G)).sum().backward()
+    h = 1e-6
+    for arr, gt, which in ((X, Xt.grad.numpy(), 0), (X2, X2t.grad.numpy(), 1)):
+        fd = np.zeros_like(arr)
+        for idx in np.ndindex(arr.shape):
+            p, m_ = arr.copy(), arr.copy()
+            p[idx] += h
+            m_[idx] -= h
+            fp = loss(p, X2) if which == 0 else loss(X, p)
+            fm = loss(m_, X2) if which == 0 else loss(X, m_)
+            fd[idx] = (fp - fm) / (2 * h)
+        np.testing.assert_allclose(gt, fd, rtol=1e-5, atol=1e-7)
