@@ -23,8 +23,8 @@ from . import ops
 
 def _check_bwd(cfg):
     if cfg["order"] != 1 or not cfg["difference"]:
-        raise NotImplementedError("gradients of the signature-kernel Gram are implemented for order=1 and "
-                                  "difference=True (gpsig_sig_gram_vjp)")
+        raise NotImplementedError("gradients of the signature kernels are implemented for order=1 and "
+                                  "difference=True (gpsig_sig_gram_vjp, gpsig_tens_vs_seq_vjp)")
 
 
 class SigGram(torch.autograd.Function):
@@ -95,3 +95,25 @@ class SigDiag(torch.autograd.Function):
         (Xs,) = ctx.saved_tensors
         gX, _ = ops.sig_gram_vjp(Xs.detach(), None, cfg["num_levels"], gout, base=cfg["base"], diag=True)
         return gX.to(Xs.dtype), None
+
+
+class TensVsSeq(torch.autograd.Function):
+    """Raw per-level inducing-tensor vs sequence kernel (SignatureKernel._K_tens_vs_seq) with a gfx950
+    backward (gpsig_tens_vs_seq_vjp) for dLoss/dZ and dLoss/dX."""
+
+    @staticmethod
+    def forward(ctx, Zs, Xs, cfg):
+        ctx.cfg = cfg
+        ctx.save_for_backward(Zs, Xs)
+        return ops.tens_vs_seq(Zs.detach(), Xs.detach(), cfg["num_levels"], cfg["order"], cfg["base"],
+                               cfg["difference"], cfg["increments"])
+
+    @staticmethod
+    def backward(ctx, gout):
+        cfg = ctx.cfg
+        _check_bwd(cfg)
+        Zs, Xs = ctx.saved_tensors
+        gZ, gX = ops.tens_vs_seq_vjp(Zs.detach(), Xs.detach(), cfg["num_levels"], gout, cfg["base"],
+                                     cfg["increments"])
+        return (gZ.to(Zs.dtype) if ctx.needs_input_grad[0] else None,
+                gX.to(Xs.dtype) if ctx.needs_input_grad[1] else None, None)

@@ -523,6 +523,16 @@ static size_t tvs_ft_bytes(int n, int l, int d) {
   return ((size_t)n * l * (2 * d + 3) * sizeof(float) + 255) & ~(size_t)255;
 }
 
+// time-major sequence features for other translation units (the tens-vs-seq VJP, sig_tvs_bwd.hip)
+namespace gpsig {
+size_t tvs_features_bytes(int n, int l, int d) { return tvs_ft_bytes(n, l, d); }
+int tvs_features_launch(const float *X, int n, int l, int d, float *Ft, hipStream_t s) {
+  const long long tot = (long long)n * l;
+  hipLaunchKernelGGL(tvs_features_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, X, n, l, d, Ft);
+  return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
+}
+}  // namespace gpsig
+
 extern "C" size_t gpsig_tens_workspace_bytes(int n, int l, int d, int lt, int t) {
   return tvs_ft_bytes(n, l, d) + tvs_pk_zp_bytes(lt, t, d);
 }

@@ -1,0 +1,304 @@
+// gpsig_amd -- gradient (vector-Jacobian product) of the inducing-tensor vs sequence kernel on gfx950.
+//
+// Forward (restated from signature_algs.py:101-127 with the seeds of kernels.py:314-341): for tensor
+// t, sequence n and level i with components c_1..c_i = k0 .. k0+i-1 (k0 = i(i-1)/2),
+//   M_k(s) = P_k(s+1) - P_k(s),  P_k(s) = k(z_k, x_s)  [increments: k(z1_k, x_s) - k(z0_k, x_s)]
+//   R_1 = M_{c_1},  R_j(s) = M_{c_j}(s) A_{j-1}(s),  A_j(s) = sum_{s'<s} R_j(s'),  K_i = sum_s R_i(s).
+// The reference gets dK/dZ, dK/dX from TF autodiff of the materialised (LT, T, N, L) tensor.  Here one
+// lane owns one (t, n) pair (64 sequences per wave, the tensor wave-uniform as in the forward kernels):
+//   * a forward sweep over time gives the end state A_j(L-1);
+//   * a reverse sweep recovers A_j(s) by inverting the update (A_j -= M A_{j-1}, ascending j) and carries
+//     the adjoints Q_j(s) = sum_{s'>s} M_{c_{j+1}}(s') Q_{j+1}(s'), Q_i = g_i = dLoss/dK_i, so that
+//     dLoss/dM_{c_j}(s) = Q_j(s) A_{j-1}(s);
+//   * the adjoint of the time difference gives dLoss/dP_k(s), and the base kernel's derivative
+//     (RBF: k (x - z) for z, k (z - x) for x; linear: x, z) the point gradients: the sequence's are
+//     added per time step (time-major, coalesced across lanes), the tensor's accumulate in registers
+//     and are reduced over the wave at the end.
+// Cells use one exp per component and time step (both sweeps evaluate the same instructions, so the
+// inversion only carries the fp32 rounding of the forward sums).
+#pragma once
+#include "sig_common.h"
+
+namespace gpsig {
+
+struct TvsBwdArgs {
+  const float *Z;     // (LT, T, d) or (LT, T, 2, d)
+  const float *Ft;    // time-major features Ft[(s * FC + c) * n + seq], FC = 2d + 3: x | dx | hdx | g | hx
+  int t, n, l, d;
+  const float *gout;  // (M+1, T, n) dLoss/dK_m (raw levels)
+  float *gZ;          // like Z, accumulated
+  float *gXt;         // (l, d, n) time-major, accumulated
+};
+
+// Level I only (levels are independent chains; blockIdx.z selects the level, so the per-lane state is
+// O(I * DP) and not O(M^2 * DP)).  LT below is the number of components of this level.
+template <int DP, int I, bool INCR, bool RBF>
+__device__ __forceinline__ void tvs_bwd_level(const TvsBwdArgs &a) {
+  constexpr int LT = I;
+  constexpr int KB = I * (I - 1) / 2;  // first component of the level
+  constexpr float NHL2E = -0.72134752044448170f;  // exp(-d2/2) = exp2(d2 * NHL2E)
+  constexpr float L2E = 1.4426950408889634f;
+  const int lane = threadIdx.x;
+  const int tt = blockIdx.y;
+  const int n = a.n, d = a.d, FC = 2 * d + 3, T = a.t, L = a.l;
+  const int s0 = blockIdx.x * 64 + lane;
+  const bool valid = s0 < n;
+  const int sq = valid ? s0 : n - 1;
+  const int zs = INCR ? 2 * d : d;
+  const float *__restrict__ Z = a.Z;
+  // component c of the level (global component KB + c)
+  auto z0c = [&](int c, int q) -> float { return q < d ? Z[((long long)(KB + c) * T + tt) * zs + q] : 0.f; };
+  auto z1c = [&](int c, int q) -> float { return q < d ? Z[((long long)(KB + c) * T + tt) * zs + d + q] : 0.f; };
+  auto ld = [&](int s, int c) -> float { return a.Ft[((long long)s * FC + c) * n + sq]; };
+  auto ldx = [&](int s, float (&x)[DP]) {
+#pragma unroll
+    for (int q = 0; q < DP; ++q) x[q] = q < d ? ld(s, q) : 0.f;
+  };
+  auto em1 = [&](float v) -> float {
+    return __builtin_fabsf(v) < EM1_TAU ? em1_small(v) : __builtin_amdgcn_exp2f(v * L2E) - 1.0f;
+  };
+  // point values of component k at x: RBF k(z0, x) [and k(z1, x)]
+  auto pvals = [&](int k, const float (&x)[DP], float &v0, float &v1) {
+    if constexpr (RBF) {
+      float e0 = 0.f, e1 = 0.f;
+#pragma unroll
+      for (int q = 0; q < DP; ++q) {
+        const float d0 = z0c(k, q) - x[q];
+        e0 = __builtin_fmaf(d0, d0, e0);
+        if constexpr (INCR) {
+          const float d1 = z1c(k, q) - x[q];
+          e1 = __builtin_fmaf(d1, d1, e1);
+        }
+      }
+      v0 = __builtin_amdgcn_exp2f(e0 * NHL2E);
+      v1 = INCR ? __builtin_amdgcn_exp2f(e1 * NHL2E) : 0.f;
+    } else {
+      v0 = v1 = 0.f;
+    }
+  };
+  // cell M_k(s) from x_s, dx_s, g_s and the point values at s (c0, c1) and s+1 (n0, n1)
+  auto cell = [&](int k, const float (&x)[DP], const float (&dx)[DP], float gs, float c0, float c1, float n0,
+                  float n1) -> float {
+    if constexpr (!RBF) {
+      float v = 0.f;
+#pragma unroll
+      for (int q = 0; q < DP; ++q) v = __builtin_fmaf(INCR ? z1c(k, q) - z0c(k, q) : z0c(k, q), dx[q], v);
+      return v;
+    } else if constexpr (!INCR) {
+      // k(z, x_{s+1}) - k(z, x_s) = k(z, x_s) expm1(<z, dx> - g)
+      float qv = -gs;
+#pragma unroll
+      for (int q = 0; q < DP; ++q) qv = __builtin_fmaf(z0c(k, q), dx[q], qv);
+      (void)n0;
+      return c0 * em1(qv);
+    } else {
+      float p = 0.f, qv = -gs, c = 0.f, hdz = 0.f;
+#pragma unroll
+      for (int q = 0; q < DP; ++q) {
+        const float z0 = z0c(k, q), dz = z1c(k, q) - z0;
+        p = __builtin_fmaf(x[q] - z0, dz, p);
+        qv = __builtin_fmaf(z0, dx[q], qv);
+        c = __builtin_fmaf(dz, dx[q], c);
+        hdz = __builtin_fmaf(dz, dz, hdz);
+      }
+      p = __builtin_fmaf(-0.5f, hdz, p);
+      const float mx = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(p), __builtin_fabsf(qv)), __builtin_fabsf(c));
+      if (mx < EM1_TAU) {
+        const float Ep = em1_small(p), Eq = em1_small(qv), Ec = em1_small(c);
+        return c0 * __builtin_fmaf(Ep, Eq, (1.0f + Ep) * (1.0f + Eq) * Ec);
+      }
+      return (n1 - n0) - (c1 - c0);
+    }
+  };
+
+  const float gI = valid ? a.gout[((long long)I * T + tt) * n + sq] : 0.f;
+
+  // ---- forward sweep: end state of the running sums A (index k0 + j - 1 for A_j of level i)
+  float A[LT], pv0[LT], pv1[LT];
+#pragma unroll
+  for (int k = 0; k < LT; ++k) A[k] = 0.f;
+  {
+    float x0[DP];
+    ldx(0, x0);
+#pragma unroll
+    for (int k = 0; k < LT; ++k) pvals(k, x0, pv0[k], pv1[k]);
+  }
+  for (int s = 0; s < L - 1; ++s) {
+    float x[DP], dx[DP], xn[DP];
+    ldx(s, x);
+#pragma unroll
+    for (int q = 0; q < DP; ++q) dx[q] = q < d ? ld(s, d + q) : 0.f;
+    ldx(s + 1, xn);
+    const float gs = ld(s, 2 * d + 1);
+    float prev = 0.f;
+#pragma unroll
+    for (int k = 0; k < I; ++k) {
+      float n0, n1;
+      pvals(k, xn, n0, n1);
+      const float m = cell(k, x, dx, gs, pv0[k], pv1[k], n0, n1);
+      pv0[k] = n0;
+      pv1[k] = n1;
+      if (k == 0) {
+        prev = m;
+      } else {
+        const float as = A[k - 1];
+        A[k - 1] = as + prev;
+        prev = m * as;
+      }
+    }
+  }
+
+  // ---- reverse sweep
+  float Acc[LT], Mh[LT];  // adjoint running sums (same indexing as A), dLoss/dM_k at the previous step
+  float S0[LT], S1[LT], V0[LT][DP], V1[LT][DP];
+#pragma unroll
+  for (int k = 0; k < LT; ++k) {
+    Acc[k] = 0.f;
+    Mh[k] = 0.f;
+    S0[k] = S1[k] = 0.f;
+#pragma unroll
+    for (int q = 0; q < DP; ++q) V0[k][q] = V1[k][q] = 0.f;
+  }
+  // point s' receives dLoss/dP_k(s') = Ph for every component k (point values v0, v1 at s')
+  auto emit = [&](int sp, const float (&Ph)[LT], const float (&v0)[LT], const float (&v1)[LT]) {
+    float xp[DP];
+    ldx(sp, xp);
+    float gxa[DP], gxs = 0.f;
+#pragma unroll
+    for (int q = 0; q < DP; ++q) gxa[q] = 0.f;
+#pragma unroll
+    for (int k = 0; k < LT; ++k) {
+      if constexpr (RBF) {
+        const float w0 = INCR ? -Ph[k] * v0[k] : Ph[k] * v0[k];
+        S0[k] += w0;
+        gxs += w0;
+#pragma unroll
+        for (int q = 0; q < DP; ++q) {
+          V0[k][q] = __builtin_fmaf(w0, xp[q], V0[k][q]);
+          gxa[q] = __builtin_fmaf(w0, z0c(k, q), gxa[q]);
+        }
+        if constexpr (INCR) {
+          const float w1 = Ph[k] * v1[k];
+          S1[k] += w1;
+          gxs += w1;
+#pragma unroll
+          for (int q = 0; q < DP; ++q) {
+            V1[k][q] = __builtin_fmaf(w1, xp[q], V1[k][q]);
+            gxa[q] = __builtin_fmaf(w1, z1c(k, q), gxa[q]);
+          }
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < DP; ++q) {
+          V0[k][q] = __builtin_fmaf(Ph[k], xp[q], V0[k][q]);
+          gxa[q] = __builtin_fmaf(Ph[k], INCR ? z1c(k, q) - z0c(k, q) : z0c(k, q), gxa[q]);
+        }
+      }
+    }
+    if (valid) {
+      for (int q = 0; q < d; ++q) {
+        const float v = RBF ? __builtin_fmaf(-gxs, xp[q], gxa[q]) : gxa[q];
+        unsafeAtomicAdd(a.gXt + ((long long)sp * d + q) * n + s0, v);
+      }
+    }
+  };
+
+  for (int s = L - 2; s >= 0; --s) {
+    float x[DP], dx[DP];
+    ldx(s, x);
+#pragma unroll
+    for (int q = 0; q < DP; ++q) dx[q] = q < d ? ld(s, d + q) : 0.f;
+    const float gs = ld(s, 2 * d + 1);
+    float c0[LT], c1[LT], Ph[LT];
+    {
+      constexpr int i = I, k0 = 0;
+      float m[I], Av[I];
+#pragma unroll
+      for (int st = 0; st < i; ++st) {
+        const int k = k0 + st;
+        pvals(k, x, c0[k], c1[k]);
+        m[st] = cell(k, x, dx, gs, c0[k], c1[k], pv0[k], pv1[k]);
+      }
+      // A_j(s) = A_j(s+1) - M_{c_j}(s) A_{j-1}(s), ascending j (A_0 = 1)
+      Av[0] = 1.0f;
+#pragma unroll
+      for (int j = 1; j < i; ++j) {
+        A[k0 + j - 1] = __builtin_fmaf(-m[j - 1], Av[j - 1], A[k0 + j - 1]);
+        Av[j] = A[k0 + j - 1];
+      }
+      // dLoss/dM_{c_j}(s) = Q_j(s) A_{j-1}(s), Q_i = g_i, Q_j = Acc (sum over s' > s)
+#pragma unroll
+      for (int j = 1; j <= i; ++j) {
+        const float Q = (j < i) ? Acc[k0 + j - 1] : gI;
+        const float mh = Q * Av[j - 1];
+        const int k = k0 + j - 1;
+        Ph[k] = mh - Mh[k];  // dLoss/dP_k(s+1) = dM_k(s) - dM_k(s+1)
+        Mh[k] = mh;
+      }
+      // Q_j(s-1) = Q_j(s) + M_{c_{j+1}}(s) Q_{j+1}(s), ascending j (old Q_{j+1})
+#pragma unroll
+      for (int j = 1; j < i; ++j) {
+        const float Qn = (j + 1 < i) ? Acc[k0 + j] : gI;
+        Acc[k0 + j - 1] = __builtin_fmaf(m[j], Qn, Acc[k0 + j - 1]);
+      }
+    }
+    emit(s + 1, Ph, pv0, pv1);
+#pragma unroll
+    for (int k = 0; k < LT; ++k) {
+      pv0[k] = c0[k];
+      pv1[k] = c1[k];
+    }
+  }
+  {
+    float Ph[LT];
+#pragma unroll
+    for (int k = 0; k < LT; ++k) Ph[k] = -Mh[k];
+    emit(0, Ph, pv0, pv1);
+  }
+
+  // ---- tensor gradients: reduce over the wave's sequences, one atomic per component channel
+  const int zoff1 = INCR ? d : 0;
+#pragma unroll
+  for (int k = 0; k < LT; ++k) {
+    float r[2 * DP + 2];
+#pragma unroll
+    for (int q = 0; q < DP; ++q) {
+      r[q] = V0[k][q];
+      r[DP + q] = V1[k][q];
+    }
+    r[2 * DP] = S0[k];
+    r[2 * DP + 1] = S1[k];
+    group_incl_scan_n<64, 2 * DP + 2>(r);
+    if (lane == 63) {
+      float *gz = a.gZ + ((long long)(KB + k) * T + tt) * zs;
+      for (int q = 0; q < d; ++q) {
+        if constexpr (RBF) {
+          unsafeAtomicAdd(gz + q, __builtin_fmaf(-r[2 * DP], z0c(k, q), r[q]));
+          if constexpr (INCR) unsafeAtomicAdd(gz + zoff1 + q, __builtin_fmaf(-r[2 * DP + 1], z1c(k, q), r[DP + q]));
+        } else if constexpr (INCR) {
+          unsafeAtomicAdd(gz + zoff1 + q, r[q]);
+          unsafeAtomicAdd(gz + q, -r[q]);
+        } else {
+          unsafeAtomicAdd(gz + q, r[q]);
+        }
+      }
+    }
+  }
+}
+
+template <int DP, int M, bool INCR, bool RBF>
+__global__ __launch_bounds__(64) void tvs_bwd_kernel(TvsBwdArgs a) {
+  switch (blockIdx.z) {
+    case 0: tvs_bwd_level<DP, 1, INCR, RBF>(a); break;
+    case 1: if constexpr (M >= 2) tvs_bwd_level<DP, 2, INCR, RBF>(a); break;
+    case 2: if constexpr (M >= 3) tvs_bwd_level<DP, 3, INCR, RBF>(a); break;
+    case 3: if constexpr (M >= 4) tvs_bwd_level<DP, 4, INCR, RBF>(a); break;
+    case 4: if constexpr (M >= 5) tvs_bwd_level<DP, 5, INCR, RBF>(a); break;
+    case 5: if constexpr (M >= 6) tvs_bwd_level<DP, 6, INCR, RBF>(a); break;
+    case 6: if constexpr (M >= 7) tvs_bwd_level<DP, 7, INCR, RBF>(a); break;
+    case 7: if constexpr (M >= 8) tvs_bwd_level<DP, 8, INCR, RBF>(a); break;
+    default: break;
+  }
+}
+
+}  // namespace gpsig

@@ -1,0 +1,37 @@
+// One (channel padding, increments) instantiation set of the tens-vs-seq VJP kernel (sig_tvs_bwd.h),
+// compiled once per -DGPSIG_DP=.. -DGPSIG_INCR=.. so the sets build in parallel.
+#include "sig_tvs_bwd.h"
+#if !defined(GPSIG_DP) || !defined(GPSIG_INCR)
+#error "GPSIG_DP and GPSIG_INCR must be defined"
+#endif
+
+namespace gpsig {
+
+template <int DP, int M, bool INCR>
+static int launch_tvs_bwd(const TvsBwdArgs &a, bool rbf, hipStream_t s) {
+  const dim3 grid((unsigned)((a.n + 63) / 64), (unsigned)a.t, (unsigned)M);
+  if (rbf)
+    hipLaunchKernelGGL((tvs_bwd_kernel<DP, M, INCR, true>), grid, dim3(64), 0, s, a);
+  else
+    hipLaunchKernelGGL((tvs_bwd_kernel<DP, M, INCR, false>), grid, dim3(64), 0, s, a);
+  return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
+}
+
+template <int DP, bool INCR>
+int tvs_bwd_launch_dp(const TvsBwdArgs &a, int M, bool rbf, hipStream_t s) {
+  switch (M) {
+    case 1: return launch_tvs_bwd<DP, 1, INCR>(a, rbf, s);
+    case 2: return launch_tvs_bwd<DP, 2, INCR>(a, rbf, s);
+    case 3: return launch_tvs_bwd<DP, 3, INCR>(a, rbf, s);
+    case 4: return launch_tvs_bwd<DP, 4, INCR>(a, rbf, s);
+    case 5: return launch_tvs_bwd<DP, 5, INCR>(a, rbf, s);
+    case 6: return launch_tvs_bwd<DP, 6, INCR>(a, rbf, s);
+    case 7: return launch_tvs_bwd<DP, 7, INCR>(a, rbf, s);
+    case 8: return launch_tvs_bwd<DP, 8, INCR>(a, rbf, s);
+    default: return GPSIG_EUNSUPPORTED;
+  }
+}
+
+template int tvs_bwd_launch_dp<GPSIG_DP, (GPSIG_INCR != 0)>(const TvsBwdArgs &, int, bool, hipStream_t);
+
+}  // namespace gpsig

@@ -215,8 +215,15 @@ class SignatureKernel:
     def _K_tens(self, Z, increments=False):
         return ops.tens_gram(Z, self.num_levels, self.base, increments)
 
+    def _rs_diff(self, Xs):
+        """1/sqrt(diag + jitter) per level, differentiable (SigDiag backward = diagonal VJP launch)."""
+        return torch.rsqrt(self._K_seq_diag(Xs) + self.jitter)
+
     def _K_tens_vs_seq(self, Z, X, increments=False):
-        return ops.tens_vs_seq(Z, X, self.num_levels, self.order, self.base, self.difference, increments)
+        """Raw per-level (num_levels+1, T, N) (kernels.py:314-341); differentiable in Z and X."""
+        cfg = self._cfg()
+        cfg["increments"] = bool(increments)
+        return _ag.TensVsSeq.apply(Z, X, cfg)
 
     def K_tens(self, Z, return_levels=False, increments=False):
         """kernels.py:544-567."""
@@ -234,8 +241,8 @@ class SignatureKernel:
         Zs = self._apply_scaling_to_incremental_tensors(Zt) if increments else self._apply_scaling_to_tensors(Zt)
         Kzx = self._K_tens_vs_seq(Zs, Xs, increments)
         if self.normalization:
-            Kzx = Kzx * self._rsqrt_diag(Xs)[:, None, :]
-        Kzx = Kzx * self._scale_vec(Xs.device)[:, None, None]
+            Kzx = Kzx * self._rs_diff(Xs)[:, None, :]
+        Kzx = Kzx * (self.sigma * self.variances).to(Xs.device, torch.float32)[:, None, None]
         return (Kzx if return_levels else Kzx.sum(0)).to(dt)
 
     def K_tens_n_seq_covs(self, Z, X, full_X_cov=False, return_levels=False, increments=False, presliced=False):

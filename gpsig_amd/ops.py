@@ -236,6 +236,32 @@ def tens_vs_seq(Z: torch.Tensor, X: torch.Tensor, num_levels: int, order: int = 
     return out
 
 
+def tens_vs_seq_vjp(Z: torch.Tensor, X: torch.Tensor, num_levels: int, gout: torch.Tensor, base="rbf",
+                    increments: bool = False, gZ: torch.Tensor | None = None, gX: torch.Tensor | None = None):
+    """dLoss/dZ, dLoss/dX of the raw per-level tens_vs_seq output (order 1, difference=True) given
+    gout (num_levels+1, T, N); accumulated into float32 buffers (see gpsig_tens_vs_seq_vjp)."""
+    _require_cuda(Z, X, gout)
+    lib = L.load()
+    Z, X = _f32(Z), _f32(X)
+    lt, t, d = Z.shape[0], Z.shape[1], Z.shape[-1]
+    n, l, dx = X.shape
+    if dx != d:
+        raise ValueError("Z and X must have the same channel count")
+    if tuple(gout.shape) != (num_levels + 1, t, n):
+        raise ValueError(f"gout must be (num_levels+1, T, N) = {(num_levels + 1, t, n)}")
+    gout = _f32(gout)
+    if gZ is None:
+        gZ = torch.zeros(Z.shape, dtype=torch.float32, device=Z.device)
+    if gX is None:
+        gX = torch.zeros(X.shape, dtype=torch.float32, device=X.device)
+    ws = workspace(X.device, lib.gpsig_tens_vjp_workspace_bytes(n, l, d))
+    rc = lib.gpsig_tens_vs_seq_vjp(Z.data_ptr(), lt, t, int(increments), d, X.data_ptr(), n, l, num_levels,
+                                   base_kind(base), gout.data_ptr(), gZ.data_ptr(), gX.data_ptr(), ws.data_ptr(),
+                                   ws.numel(), _stream(X.device))
+    L.check(rc, "gpsig_tens_vs_seq_vjp")
+    return gZ, gX
+
+
 def tens_gram(Z: torch.Tensor, num_levels: int, base="rbf", increments: bool = False) -> torch.Tensor:
     """Inducing-tensor Gram per level: Z (LT,T,D) or (LT,T,2,D) -> (M+1, T, T)."""
     _require_cuda(Z)

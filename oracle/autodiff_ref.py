@@ -93,3 +93,44 @@ def K(Xs, X2s, num_levels, base="rbf", normalization=True, scale=None, jitter=1e
         scale = torch.ones(num_levels + 1, dtype=K_l.dtype)
     K_l = K_l * scale[:, None, None]
     return K_l if return_levels else K_l.sum(0)
+
+
+def tens_vs_seq_first_order(M: torch.Tensor, num_levels: int, difference: bool = True) -> torch.Tensor:
+    """signature_algs.py:101-127: M (LT, T, N, L) -> (num_levels+1, T, N)."""
+    if difference:
+        M = M[..., 1:] - M[..., :-1]
+    K = [torch.ones((M.shape[1], M.shape[2]), dtype=M.dtype)]
+    k = 0
+    for i in range(1, num_levels + 1):
+        R = M[k]
+        k += 1
+        for _ in range(1, i):
+            R = M[k] * _xcumsum(R, 2)
+            k += 1
+        K.append(R.sum(2))
+    return torch.stack(K, 0)
+
+
+def k_tens_vs_seq(Zs, Xs, num_levels, base="rbf", increments=False, difference=True):
+    """_K_tens_vs_seq (kernels.py:314-341): Zs (LT,T,d) or (LT,T,2,d), Xs (N,L,d) -> (M+1, T, N) raw."""
+    LT, T, d = Zs.shape[0], Zs.shape[1], Zs.shape[-1]
+    N, L = Xs.shape[0], Xs.shape[1]
+    Xf = Xs.reshape(N * L, d)
+    if increments:
+        M = base_kern(Zs.reshape(2 * T * LT, d), Xf, base).reshape(LT, T, 2, N, L)
+        M = M[:, :, 1] - M[:, :, 0]
+    else:
+        M = base_kern(Zs.reshape(T * LT, d), Xf, base).reshape(LT, T, N, L)
+    return tens_vs_seq_first_order(M, num_levels, difference)
+
+
+def K_tens_vs_seq(Zs, Xs, num_levels, base="rbf", increments=False, normalization=True, scale=None, jitter=1e-6,
+                  return_levels=False):
+    """SignatureKernel.K_tens_vs_seq (kernels.py:571-620) on scaled tensors / sequences."""
+    Kzx = k_tens_vs_seq(Zs, Xs, num_levels, base, increments)
+    if normalization:
+        Kzx = Kzx / torch.sqrt(k_seq_diag(Xs, num_levels, base) + jitter)[:, None, :]
+    if scale is None:
+        scale = torch.ones(num_levels + 1, dtype=Kzx.dtype)
+    Kzx = Kzx * scale[:, None, None]
+    return Kzx if return_levels else Kzx.sum(0)

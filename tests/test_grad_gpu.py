@@ -146,3 +146,38 @@ def test_raw_levels_vjp_ragged_lengths(base):
     (ar.k_seq(Xr, Yr, M, base) * torch.tensor(G)).sum().backward()
     assert norm_rel_err(gX.cpu().numpy(), Xr.grad.numpy()) < GTOL
     assert norm_rel_err(gY.cpu().numpy(), Yr.grad.numpy()) < GTOL
+
+
+@pytest.mark.parametrize("base", ["rbf", "linear"])
+@pytest.mark.parametrize("increments", [False, True])
+@pytest.mark.parametrize("M,D,L", [(3, 3, 20), (5, 5, 40), (1, 2, 9), (8, 8, 12)])
+def test_tens_vs_seq_vjp_matches_autodiff(base, increments, M, D, L):
+    """K_tens_vs_seq (normalised, summed) gradients in Z, X, lengthscales, variances."""
+    import gpsig_amd
+    T, N = 7, 70  # N > 64: two sequence blocks, a partial one
+    LT = M * (M + 1) // 2
+    rng = np.random.default_rng(20 + M)
+    Z = 0.5 * rng.standard_normal((LT, T, 2, D) if increments else (LT, T, D))
+    X = walks(N, L, D, 21)
+    G = rng.standard_normal((T, N))
+    ls = 0.8 + 0.4 * rng.random(D)
+    cls = gpsig_amd.SignatureRBF if base == "rbf" else gpsig_amd.SignatureLinear
+    k = cls(L * D, D, M)
+    k.lengthscales = torch.tensor(ls, device=DEV, requires_grad=True)
+    k.variances = torch.tensor(np.linspace(0.5, 1.5, M + 1), device=DEV, requires_grad=True)
+    Zt = torch.tensor(Z, device=DEV, requires_grad=True)
+    Xt = torch.tensor(X.reshape(N, -1), device=DEV, requires_grad=True)
+    K = k.K_tens_vs_seq(Zt, Xt, increments=increments)
+    (K * torch.as_tensor(G, device=DEV)).sum().backward()
+
+    Zr, Xr = torch.tensor(Z, requires_grad=True), torch.tensor(X, requires_grad=True)
+    lr = torch.tensor(ls, requires_grad=True)
+    vr = torch.tensor(np.linspace(0.5, 1.5, M + 1), requires_grad=True)
+    Zs = Zr / lr
+    Kr = ar.K_tens_vs_seq(Zs, Xr / lr, M, base=base, increments=increments, scale=vr)
+    (Kr * torch.tensor(G)).sum().backward()
+    assert norm_rel_err(K.detach().cpu().numpy(), Kr.detach().numpy()) < 1e-5
+    assert norm_rel_err(Zt.grad.cpu().numpy(), Zr.grad.numpy()) < GTOL
+    assert norm_rel_err(Xt.grad.reshape(X.shape).cpu().numpy(), Xr.grad.numpy()) < GTOL
+    assert norm_rel_err(k.lengthscales.grad.cpu().numpy(), lr.grad.numpy()) < GTOL
+    assert norm_rel_err(k.variances.grad.cpu().numpy(), vr.grad.numpy()) < GTOL

@@ -59,3 +59,34 @@ def test_autodiff_oracle_gradient_matches_finite_differences(base):
             fm = loss(m_, X2) if which == 0 else loss(X, m_)
             fd[idx] = (fp - fm) / (2 * h)
         np.testing.assert_allclose(gt, fd, rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("base", ["rbf", "linear"])
+@pytest.mark.parametrize("increments", [False, True])
+def test_autodiff_oracle_tens_vs_seq(base, increments):
+    """Forward equals the NumPy oracle; dLoss/dZ and dLoss/dX equal central differences of it."""
+    M, T, N, L, D = 3, 2, 3, 5, 2
+    LT = M * (M + 1) // 2
+    rng = np.random.default_rng(7)
+    Z = 0.5 * rng.standard_normal((LT, T, 2, D) if increments else (LT, T, D))
+    X = walks(N, L, D, 8)
+    k = kr.SignatureKernelRef(L * D, D, M, base=base)
+    ref = k.K_tens_vs_seq(Z, X.reshape(N, -1), return_levels=True, increments=increments)
+    Zt, Xt = torch.tensor(Z, requires_grad=True), torch.tensor(X, requires_grad=True)
+    got = ar.K_tens_vs_seq(Zt, Xt, M, base=base, increments=increments, return_levels=True)
+    np.testing.assert_allclose(got.detach().numpy(), ref, rtol=1e-11, atol=1e-13)
+    G = rng.standard_normal((T, N))
+    (ar.K_tens_vs_seq(Zt, Xt, M, base=base, increments=increments) * torch.tensor(G)).sum().backward()
+
+    def loss(Zv, Xv):
+        return float((k.K_tens_vs_seq(Zv, Xv.reshape(N, -1), increments=increments) * G).sum())
+
+    h = 1e-6
+    for arr, gt, which in ((Z, Zt.grad.numpy(), 0), (X, Xt.grad.numpy(), 1)):
+        fd = np.zeros_like(arr)
+        for idx in np.ndindex(arr.shape):
+            p, m_ = arr.copy(), arr.copy()
+            p[idx] += h
+            m_[idx] -= h
+            fd[idx] = ((loss(p, X) - loss(m_, X)) if which == 0 else (loss(Z, p) - loss(Z, m_))) / (2 * h)
+        np.testing.assert_allclose(gt, fd, rtol=1e-5, atol=1e-7)
