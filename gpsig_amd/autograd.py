@@ -117,3 +117,54 @@ class TensVsSeq(torch.autograd.Function):
                                      cfg["increments"])
         return (gZ.to(Zs.dtype) if ctx.needs_input_grad[0] else None,
                 gX.to(Xs.dtype) if ctx.needs_input_grad[1] else None, None)
+
+
+class TensGram(torch.autograd.Function):
+    """Raw per-level inducing-tensor Gram (SignatureKernel._K_tens) with a gfx950 backward
+    (gpsig_tens_gram_vjp) for dLoss/dZ."""
+
+    @staticmethod
+    def forward(ctx, Zs, cfg):
+        ctx.cfg = cfg
+        ctx.save_for_backward(Zs)
+        return ops.tens_gram(Zs.detach(), cfg["num_levels"], cfg["base"], cfg["increments"])
+
+    @staticmethod
+    def backward(ctx, gout):
+        cfg = ctx.cfg
+        (Zs,) = ctx.saved_tensors
+        gZ = ops.tens_gram_vjp(Zs.detach(), cfg["num_levels"], gout, cfg["base"], cfg["increments"])
+        return gZ.to(Zs.dtype), None
+
+
+class PdeDiag(torch.autograd.Function):
+    """k(x_a, x_a) of the Goursat PDE (UntruncSignatureKernel.Kdiag) with the reference's adjoint
+    (kernels_pde.py:465-509) as backward (gpsig_pde_vjp, DIAG)."""
+
+    @staticmethod
+    def forward(ctx, Xs, dyadic, solver):
+        ctx.dyadic, ctx.solver = dyadic, solver
+        ctx.save_for_backward(Xs)
+        return ops.pde_diag(Xs.detach(), dyadic, solver)
+
+    @staticmethod
+    def backward(ctx, gout):
+        (Xs,) = ctx.saved_tensors
+        gX = ops.pde_diag_vjp(Xs.detach(), gout, ctx.dyadic, ctx.solver)
+        return gX.to(Xs.dtype), None, None
+
+
+class PdeGram(torch.autograd.Function):
+    """PDE cross Gram (UntruncSignatureKernel.K) with the same adjoint extended to cross pairs."""
+
+    @staticmethod
+    def forward(ctx, Xs, X2s, dyadic, solver):
+        ctx.dyadic, ctx.solver = dyadic, solver
+        ctx.save_for_backward(Xs, X2s)
+        return ops.pde_gram(Xs.detach(), None if X2s is None else X2s.detach(), dyadic, solver)
+
+    @staticmethod
+    def backward(ctx, gout):
+        Xs, X2s = ctx.saved_tensors
+        gX, gY = ops.pde_gram_vjp(Xs.detach(), None if X2s is None else X2s.detach(), gout, ctx.dyadic, ctx.solver)
+        return (gX.to(Xs.dtype), None if gY is None else gY.to(X2s.dtype), None, None)

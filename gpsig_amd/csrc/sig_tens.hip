@@ -588,6 +588,134 @@ extern "C" int gpsig_tens_gram(const float *Z, int lt, int t, int increments, in
   return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
 }
 
+// ------------------------------------------------------------------------------------ tensor Gram VJP
+// Gradient of tensor_kern (signature_algs.py:76-99) over the component Grams of _K_tens
+// (kernels.py:264-284): K_i(t, t') = prod_{c in level i} M_c(t, t'), so
+//   dLoss/dz_c^t = sum_t' (G_i(t, t') + G_i(t', t)) prod_{c' != c} M_c'(t, t') d/dz_c^t M_c(t, t')
+// (the symmetric sum covers t as the second argument).  Lane = t, block = (level, chunk of t').
+struct TgBwdArgs {
+  const float *Z;     // (LT, T, d) or (LT, T, 2, d)
+  int t, d, incr, rbf, chunk;
+  const float *gout;  // (M+1, T, T)
+  float *gZ;          // like Z, accumulated
+};
+
+template <int DP>
+__global__ __launch_bounds__(64) void tens_gram_vjp_kernel(TgBwdArgs a) {
+  const int t1 = blockIdx.x * 64 + threadIdx.x;
+  if (t1 >= a.t) return;
+  const int i = blockIdx.y + 1, k0 = i * (i - 1) / 2;
+  const int tb = blockIdx.z * a.chunk, te = min(a.t, tb + a.chunk);
+  const int d = a.d, T = a.t, zs = a.incr ? 2 * d : d;
+  auto zv = [&](int k, int tt, int h, int q) -> float {
+    return q < d ? a.Z[((long long)k * T + tt) * zs + h * d + q] : 0.f;
+  };
+  float g0[TV_MMAX][DP], g1[TV_MMAX][DP];
+#pragma unroll
+  for (int c = 0; c < TV_MMAX; ++c)
+#pragma unroll
+    for (int q = 0; q < DP; ++q) g0[c][q] = g1[c][q] = 0.f;
+  for (int t2 = tb; t2 < te; ++t2) {
+    const float Gs = a.gout[((long long)i * T + t1) * T + t2] + a.gout[((long long)i * T + t2) * T + t1];
+    float m[TV_MMAX];
+#pragma unroll
+    for (int c = 0; c < TV_MMAX; ++c) {
+      if (c >= i) break;
+      const int k = k0 + c;
+      if (!a.incr) {
+        float s2 = 0.f, ip = 0.f;
+#pragma unroll
+        for (int q = 0; q < DP; ++q) {
+          const float df = zv(k, t1, 0, q) - zv(k, t2, 0, q);
+          s2 = __builtin_fmaf(df, df, s2);
+          ip = __builtin_fmaf(zv(k, t1, 0, q), zv(k, t2, 0, q), ip);
+        }
+        m[c] = a.rbf ? fast_exp(-0.5f * s2) : ip;
+      } else {
+        float A0[DP], dA[DP], B0[DP], dB[DP];
+#pragma unroll
+        for (int q = 0; q < DP; ++q) {
+          A0[q] = zv(k, t1, 0, q);
+          dA[q] = zv(k, t1, 1, q) - A0[q];
+          B0[q] = zv(k, t2, 0, q);
+          dB[q] = zv(k, t2, 1, q) - B0[q];
+        }
+        if (a.rbf) {
+          m[c] = rbf_second_diff<DP>(A0, dA, B0, dB);
+        } else {
+          float v = 0.f;
+#pragma unroll
+          for (int q = 0; q < DP; ++q) v = __builtin_fmaf(dA[q], dB[q], v);
+          m[c] = v;
+        }
+      }
+    }
+    // products of the other components: prefix * suffix
+    float pre[TV_MMAX], suf = 1.f;
+    pre[0] = 1.f;
+#pragma unroll
+    for (int c = 1; c < TV_MMAX; ++c) pre[c] = (c < i) ? pre[c - 1] * m[c - 1] : 0.f;
+#pragma unroll
+    for (int c = TV_MMAX - 1; c >= 0; --c) {
+      if (c >= i) continue;
+      const float w = Gs * pre[c] * suf;
+      suf *= m[c];
+      const int k = k0 + c;
+      if (!a.incr) {
+        if (a.rbf) {
+          float s2 = 0.f;
+#pragma unroll
+          for (int q = 0; q < DP; ++q) {
+            const float df = zv(k, t2, 0, q) - zv(k, t1, 0, q);
+            s2 = __builtin_fmaf(df, df, s2);
+          }
+          const float wk = w * fast_exp(-0.5f * s2);
+#pragma unroll
+          for (int q = 0; q < DP; ++q) g0[c][q] = __builtin_fmaf(wk, zv(k, t2, 0, q) - zv(k, t1, 0, q), g0[c][q]);
+        } else {
+#pragma unroll
+          for (int q = 0; q < DP; ++q) g0[c][q] = __builtin_fmaf(w, zv(k, t2, 0, q), g0[c][q]);
+        }
+      } else if (a.rbf) {
+        // dM/dA1 = k(A1,B1)(B1 - A1) - k(A1,B0)(B0 - A1),  dM/dA0 = k(A0,B0)(B0 - A0) - k(A0,B1)(B1 - A0)
+        float e11 = 0.f, e10 = 0.f, e00 = 0.f, e01 = 0.f;
+#pragma unroll
+        for (int q = 0; q < DP; ++q) {
+          const float a0 = zv(k, t1, 0, q), a1 = zv(k, t1, 1, q), b0 = zv(k, t2, 0, q), b1 = zv(k, t2, 1, q);
+          e11 = __builtin_fmaf(a1 - b1, a1 - b1, e11);
+          e10 = __builtin_fmaf(a1 - b0, a1 - b0, e10);
+          e00 = __builtin_fmaf(a0 - b0, a0 - b0, e00);
+          e01 = __builtin_fmaf(a0 - b1, a0 - b1, e01);
+        }
+        const float k11 = w * fast_exp(-0.5f * e11), k10 = w * fast_exp(-0.5f * e10);
+        const float k00 = w * fast_exp(-0.5f * e00), k01 = w * fast_exp(-0.5f * e01);
+#pragma unroll
+        for (int q = 0; q < DP; ++q) {
+          const float a0 = zv(k, t1, 0, q), a1 = zv(k, t1, 1, q), b0 = zv(k, t2, 0, q), b1 = zv(k, t2, 1, q);
+          g1[c][q] += k11 * (b1 - a1) - k10 * (b0 - a1);
+          g0[c][q] += k00 * (b0 - a0) - k01 * (b1 - a0);
+        }
+      } else {
+#pragma unroll
+        for (int q = 0; q < DP; ++q) {
+          const float dBq = zv(k, t2, 1, q) - zv(k, t2, 0, q);
+          g1[c][q] = __builtin_fmaf(w, dBq, g1[c][q]);
+          g0[c][q] = __builtin_fmaf(-w, dBq, g0[c][q]);
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < TV_MMAX; ++c) {
+    if (c >= i) break;
+    float *gz = a.gZ + ((long long)(k0 + c) * T + t1) * zs;
+    for (int q = 0; q < d; ++q) {
+      unsafeAtomicAdd(gz + q, g0[c][q]);
+      if (a.incr) unsafeAtomicAdd(gz + d + q, g1[c][q]);
+    }
+  }
+}
+
 template <int M, int W>
 static int launch_rs(const RsArgs &a, int DP, hipStream_t s) {
   dim3 grid(a.t + 1, a.n);
@@ -637,5 +765,26 @@ extern "C" int gpsig_rescaled(const float *Z, int lt, int t, const float *X, int
   const long long tot = (long long)num_levels * n * t;
   hipLaunchKernelGGL(rescaled_combine_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, out, a.kones,
                      num_levels, n, t);
+  return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
+}
+
+extern "C" int gpsig_tens_gram_vjp(const float *Z, int lt, int t, int increments, int d, int num_levels,
+                                   int base_kind, const float *gout, float *gZ, gpsig_stream_t stream) {
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (!Z || !gout || !gZ || lt <= 0 || t <= 0 || d <= 0 || num_levels < 1) return GPSIG_EINVAL;
+  if (lt != num_levels * (num_levels + 1) / 2) return GPSIG_EINVAL;
+  if (num_levels > TV_MMAX) return GPSIG_EUNSUPPORTED;
+  if (base_kind != GPSIG_BASE_RBF && base_kind != GPSIG_BASE_LINEAR) return GPSIG_EUNSUPPORTED;
+  const int DP = dpad4(d);
+  if (DP == 0) return GPSIG_EUNSUPPORTED;
+  const int chunk = 64;
+  TgBwdArgs a{Z, t, d, increments, base_kind == GPSIG_BASE_RBF, chunk, gout, gZ};
+  dim3 grid((t + 63) / 64, num_levels, (t + chunk - 1) / chunk);
+  switch (DP) {
+    case 4: hipLaunchKernelGGL(tens_gram_vjp_kernel<4>, grid, dim3(64), 0, s, a); break;
+    case 8: hipLaunchKernelGGL(tens_gram_vjp_kernel<8>, grid, dim3(64), 0, s, a); break;
+    case 16: hipLaunchKernelGGL(tens_gram_vjp_kernel<16>, grid, dim3(64), 0, s, a); break;
+    default: hipLaunchKernelGGL(tens_gram_vjp_kernel<32>, grid, dim3(64), 0, s, a); break;
+  }
   return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
 }

@@ -213,7 +213,10 @@ class SignatureKernel:
 
     # ------------------------------------------------------------------ inducing tensors (kernels.py:544-704)
     def _K_tens(self, Z, increments=False):
-        return ops.tens_gram(Z, self.num_levels, self.base, increments)
+        """Raw per-level (num_levels+1, T, T) (kernels.py:264-284); differentiable in Z."""
+        cfg = self._cfg()
+        cfg["increments"] = bool(increments)
+        return _ag.TensGram.apply(Z, cfg)
 
     def _rs_diff(self, Xs):
         """1/sqrt(diag + jitter) per level, differentiable (SigDiag backward = diagonal VJP launch)."""
@@ -230,7 +233,7 @@ class SignatureKernel:
         Zt = _as_tensor(Z)
         dt = self._out_dtype(Z)
         Zs = self._apply_scaling_to_incremental_tensors(Zt) if increments else self._apply_scaling_to_tensors(Zt)
-        K = self._K_tens(Zs, increments) * self._scale_vec(Zs.device)[:, None, None]
+        K = self._K_tens(Zs, increments) * (self.sigma * self.variances).to(Zs.device, torch.float32)[:, None, None]
         return (K if return_levels else K.sum(0)).to(dt)
 
     def K_tens_vs_seq(self, Z, X, return_levels=False, increments=False, presliced=False):

@@ -19,6 +19,7 @@ from __future__ import annotations
 import numpy as np
 import torch
 
+from . import autograd as _ag
 from . import lags as _lags
 from . import ops
 from .kernels import DEFAULT_JITTER, _as_tensor, _tensor_inner_product, _tensor_logs
@@ -47,6 +48,7 @@ class UntruncSignatureKernel:
         self.sigma = torch.tensor(1.0, dtype=torch.float64)
         self.num_levels = num_levels
         self.jitter = float(jitter)
+        self.solver = 1  # the explicit scheme of both reference paths (sigKer_fast.pyx:48, .cu:29)
         if num_lags is None:
             self.num_lags = 0
         else:
@@ -100,13 +102,14 @@ class UntruncSignatureKernel:
     def Kdiag(self, X, presliced=False, name=None):
         """kernels_pde.py:160-185: sigma * k(x, x) from the PDE solve, (N,)."""
         Xs = self._prep(X)
-        return (float(self.sigma) * ops.pde_diag(Xs, self.order, 1)).to(self._dt(X))
+        # differentiable: backward = the reference's adjoint (kernels_pde.py:465-509) on gfx950
+        return (float(self.sigma) * _ag.PdeDiag.apply(Xs, self.order, self.solver)).to(self._dt(X))
 
     def K(self, X, X2=None, presliced=False):
         """New: sigma * k(x_a, y_b) PDE cross Gram, (N, N2)."""
         Xs = self._prep(X)
         X2s = None if X2 is None else self._prep(X2)
-        return (float(self.sigma) * ops.pde_gram(Xs, X2s, self.order, 1)).to(self._dt(X))
+        return (float(self.sigma) * _ag.PdeGram.apply(Xs, X2s, self.order, self.solver)).to(self._dt(X))
 
     def compute_K(self, X, Y):
         return self.K(_as_tensor(X), _as_tensor(Y)).cpu().numpy()

@@ -197,6 +197,54 @@ def pde_gram(X: torch.Tensor, Y: torch.Tensor | None = None, dyadic: int = 0, so
     return out
 
 
+PDE_VJP_SCRATCH = 1 << 30  # bytes of fp64 K_rev grids per launch (rows are chunked to fit)
+
+
+def pde_diag_vjp(X: torch.Tensor, gout: torch.Tensor, dyadic: int = 0, solver: int = 1,
+                 gX: torch.Tensor | None = None) -> torch.Tensor:
+    """dLoss/dX of pde_diag (the reference's _KdiagGrad adjoint, kernels_pde.py:465-509) given gout (n,)."""
+    _require_cuda(X, gout)
+    lib = L.load()
+    X, gout = _f32(X), _f32(gout)
+    n, l, d = X.shape
+    if gX is None:
+        gX = torch.zeros((n, l, d), dtype=torch.float32, device=X.device)
+    per = lib.gpsig_pde_vjp_workspace_bytes(1, l, l, dyadic)
+    step = max(1, min(n, PDE_VJP_SCRATCH // max(per, 1)))
+    for r0 in range(0, n, step):
+        r1 = min(n, r0 + step)
+        ws = workspace(X.device, lib.gpsig_pde_vjp_workspace_bytes(r1 - r0, l, l, dyadic))
+        rc = lib.gpsig_pde_vjp(X.data_ptr(), n, l, X.data_ptr(), n, l, d, dyadic, solver, L.PAIRS_DIAG, r0, r1,
+                               gout.data_ptr(), gX.data_ptr(), None, ws.data_ptr(), ws.numel(), _stream(X.device))
+        L.check(rc, "gpsig_pde_vjp")
+    return gX
+
+
+def pde_gram_vjp(X: torch.Tensor, Y: torch.Tensor | None, gout: torch.Tensor, dyadic: int = 0, solver: int = 1):
+    """(dLoss/dX, dLoss/dY) of pde_gram given gout (n1, n2) (Y None: symmetric K(X), returns (gX, None))."""
+    _require_cuda(X, Y, gout)
+    lib = L.load()
+    X, gout = _f32(X), _f32(gout)
+    sym = Y is None
+    Y = X if sym else _f32(Y)
+    n1, l1, d = X.shape
+    n2, l2, _ = Y.shape
+    if tuple(gout.shape) != (n1, n2):
+        raise ValueError(f"gout must be {(n1, n2)}")
+    gX = torch.zeros((n1, l1, d), dtype=torch.float32, device=X.device)
+    gY = gX if sym else torch.zeros((n2, l2, d), dtype=torch.float32, device=X.device)
+    per = lib.gpsig_pde_vjp_workspace_bytes(n2, l1, l2, dyadic)
+    step = max(4, (min(n1, PDE_VJP_SCRATCH // max(per, 1)) // 4) * 4)
+    for r0 in range(0, n1, step):
+        r1 = min(n1, r0 + step)
+        ws = workspace(X.device, lib.gpsig_pde_vjp_workspace_bytes((r1 - r0) * n2, l1, l2, dyadic))
+        rc = lib.gpsig_pde_vjp(X.data_ptr(), n1, l1, Y.data_ptr(), n2, l2, d, dyadic, solver, L.PAIRS_RECT, r0, r1,
+                               gout.data_ptr(), gX.data_ptr(), gY.data_ptr(), ws.data_ptr(), ws.numel(),
+                               _stream(X.device))
+        L.check(rc, "gpsig_pde_vjp")
+    return gX, (None if sym else gY)
+
+
 # ----------------------------------------------------------------------------- multi-GPU helper
 def sym_assemble(src: torch.Tensor, row_off: torch.Tensor, level_stride: int, n: int, levels: int,
                  out: torch.Tensor | None = None) -> torch.Tensor:
@@ -273,6 +321,24 @@ def tens_gram(Z: torch.Tensor, num_levels: int, base="rbf", increments: bool = F
                              _stream(Z.device))
     L.check(rc, "gpsig_tens_gram")
     return out
+
+
+def tens_gram_vjp(Z: torch.Tensor, num_levels: int, gout: torch.Tensor, base="rbf", increments: bool = False,
+                  gZ: torch.Tensor | None = None) -> torch.Tensor:
+    """dLoss/dZ of the raw per-level tensor Gram given gout (num_levels+1, T, T) (gpsig_tens_gram_vjp)."""
+    _require_cuda(Z, gout)
+    lib = L.load()
+    Z = _f32(Z)
+    lt, t, d = Z.shape[0], Z.shape[1], Z.shape[-1]
+    if tuple(gout.shape) != (num_levels + 1, t, t):
+        raise ValueError(f"gout must be (num_levels+1, T, T) = {(num_levels + 1, t, t)}")
+    gout = _f32(gout)
+    if gZ is None:
+        gZ = torch.zeros(Z.shape, dtype=torch.float32, device=Z.device)
+    rc = lib.gpsig_tens_gram_vjp(Z.data_ptr(), lt, t, int(increments), d, num_levels, base_kind(base), gout.data_ptr(),
+                                 gZ.data_ptr(), _stream(Z.device))
+    L.check(rc, "gpsig_tens_gram_vjp")
+    return gZ
 
 
 EMBEDDINGS = {"linear": 0, "rbf": 1}

@@ -137,6 +137,11 @@ int gpsig_tens_vs_seq(const float *Z, int lt, int t, int increments, int d, cons
 int gpsig_tens_gram(const float *Z, int lt, int t, int increments, int d, int num_levels, int base_kind, float *out,
                     gpsig_stream_t stream);
 
+/* Gradient of gpsig_tens_gram (tensor_kern, signature_algs.py:76-99, over _K_tens, kernels.py:264-284):
+ * gout (num_levels+1, T, T) = dLoss/d(raw per-level output); accumulates (+=) gZ (same layout as Z). */
+int gpsig_tens_gram_vjp(const float *Z, int lt, int t, int increments, int d, int num_levels, int base_kind,
+                        const float *gout, float *gZ, gpsig_stream_t stream);
+
 /* Gradient of gpsig_tens_vs_seq (order 1, difference = True, RBF or linear, num_levels <= 8, d <= 8):
  * the reference differentiates _K_tens_vs_seq (kernels.py:314-341 + signature_algs.py:101-127) by TF
  * autodiff.  gout (num_levels+1, T, n) = dLoss/d(raw per-level output); accumulates (+=) gZ (same
@@ -167,6 +172,19 @@ int gpsig_pde_gram(const float *X, int n1, int l1, const float *Y, int n2, int l
                    gpsig_stream_t stream);
 
 int gpsig_pde_diag(const float *X, int n, int l, int d, int dyadic, int solver, float *out, gpsig_stream_t stream);
+
+/* Gradient of gpsig_pde_gram / gpsig_pde_diag: the reference's own adjoint (kernels_pde.py:465-509,
+ * _KdiagGrad; covariance_op/_untrunc_cov_grad.py:25-77): KK = K (.) flip(K_rev) with K_rev solved on the
+ * time-reversed paths by the first-order scheme, contracted with the increments.  pair_mode DIAG
+ * (gout (n1,), dLoss/dk(x_a, x_a); the reference's factor 2 for the symmetric pair) or RECT (gout
+ * (n1, n2); gX and gY).  Accumulates (+=) gX (n1, l1, d), gY (n2, l2, d).  Workspace: one fp64
+ * (2^dyadic (l1-1) + 1) x (2^dyadic (l2-1) + 1) grid per evaluated pair,
+ * gpsig_pde_vjp_workspace_bytes(pairs, l1, l2, dyadic). */
+size_t gpsig_pde_vjp_workspace_bytes(int npairs, int l1, int l2, int dyadic);
+
+int gpsig_pde_vjp(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int dyadic, int solver,
+                  int pair_mode, int row_begin, int row_end, const float *gout, float *gX, float *gY, void *workspace,
+                  size_t workspace_bytes, gpsig_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Multi-GPU assembly helper (no reference counterpart: the reference has no distributed code).

@@ -134,3 +134,24 @@ def K_tens_vs_seq(Zs, Xs, num_levels, base="rbf", increments=False, normalizatio
         scale = torch.ones(num_levels + 1, dtype=Kzx.dtype)
     Kzx = Kzx * scale[:, None, None]
     return Kzx if return_levels else Kzx.sum(0)
+
+
+def k_tens(Zs, num_levels, base="rbf", increments=False):
+    """_K_tens (kernels.py:264-284) + tensor_kern (signature_algs.py:76-99): (M+1, T, T) raw."""
+    LT, T, d = Zs.shape[0], Zs.shape[1], Zs.shape[-1]
+    if increments:
+        Zr = Zs.reshape(LT, 2 * T, d)
+        M = torch.stack([base_kern(Zr[c], Zr[c], base) for c in range(LT)], 0).reshape(LT, T, 2, T, 2)
+        M = M[:, :, 1, :, 1] + M[:, :, 0, :, 0] - M[:, :, 1, :, 0] - M[:, :, 0, :, 1]
+    else:
+        M = torch.stack([base_kern(Zs[c], Zs[c], base) for c in range(LT)], 0)
+    K = [torch.ones((T, T), dtype=Zs.dtype)]
+    k = 0
+    for i in range(1, num_levels + 1):
+        R = M[k]
+        k += 1
+        for _ in range(1, i):
+            R = M[k] * R
+            k += 1
+        K.append(R)
+    return torch.stack(K, 0)

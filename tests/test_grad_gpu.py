@@ -181,3 +181,28 @@ def test_tens_vs_seq_vjp_matches_autodiff(base, increments, M, D, L):
     assert norm_rel_err(Xt.grad.reshape(X.shape).cpu().numpy(), Xr.grad.numpy()) < GTOL
     assert norm_rel_err(k.lengthscales.grad.cpu().numpy(), lr.grad.numpy()) < GTOL
     assert norm_rel_err(k.variances.grad.cpu().numpy(), vr.grad.numpy()) < GTOL
+
+
+@pytest.mark.parametrize("base", ["rbf", "linear"])
+@pytest.mark.parametrize("increments", [False, True])
+def test_tens_gram_vjp_matches_autodiff(base, increments):
+    """K_tens (Kzz, summed over levels x sigma*variances) gradients in Z and lengthscales."""
+    import gpsig_amd
+    M, T, D = 4, 70, 3
+    LT = M * (M + 1) // 2
+    rng = np.random.default_rng(30)
+    Z = 0.5 * rng.standard_normal((LT, T, 2, D) if increments else (LT, T, D))
+    G = rng.standard_normal((T, T))
+    ls = np.array([0.9, 1.1, 1.3])
+    cls = gpsig_amd.SignatureRBF if base == "rbf" else gpsig_amd.SignatureLinear
+    k = cls(10 * D, D, M)
+    k.lengthscales = torch.tensor(ls, device=DEV, requires_grad=True)
+    Zt = torch.tensor(Z, device=DEV, requires_grad=True)
+    K = k.K_tens(Zt, increments=increments)
+    (K * torch.as_tensor(G, device=DEV)).sum().backward()
+    Zr, lr = torch.tensor(Z, requires_grad=True), torch.tensor(ls, requires_grad=True)
+    Kr = ar.k_tens(Zr / lr, M, base, increments).sum(0)
+    (Kr * torch.tensor(G)).sum().backward()
+    assert norm_rel_err(K.detach().cpu().numpy(), Kr.detach().numpy()) < 1e-5
+    assert norm_rel_err(Zt.grad.cpu().numpy(), Zr.grad.numpy()) < GTOL
+    assert norm_rel_err(k.lengthscales.grad.cpu().numpy(), lr.grad.numpy()) < GTOL

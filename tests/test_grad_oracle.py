@@ -90,3 +90,26 @@ def test_autodiff_oracle_tens_vs_seq(base, increments):
             m_[idx] -= h
             fd[idx] = ((loss(p, X) - loss(m_, X)) if which == 0 else (loss(Z, p) - loss(Z, m_))) / (2 * h)
         np.testing.assert_allclose(gt, fd, rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("base", ["rbf", "linear"])
+@pytest.mark.parametrize("increments", [False, True])
+def test_autodiff_oracle_tens_gram(base, increments):
+    M, T, D = 3, 4, 2
+    LT = M * (M + 1) // 2
+    rng = np.random.default_rng(9)
+    Z = 0.5 * rng.standard_normal((LT, T, 2, D) if increments else (LT, T, D))
+    k = kr.SignatureKernelRef(2 * D, D, M, base=base)
+    ref = k.K_tens_raw(Z, increments)
+    Zt = torch.tensor(Z, requires_grad=True)
+    np.testing.assert_allclose(ar.k_tens(Zt, M, base, increments).detach().numpy(), ref, rtol=1e-11, atol=1e-13)
+    G = rng.standard_normal((M + 1, T, T))
+    (ar.k_tens(Zt, M, base, increments) * torch.tensor(G)).sum().backward()
+    h = 1e-6
+    fd = np.zeros_like(Z)
+    for idx in np.ndindex(Z.shape):
+        p, m_ = Z.copy(), Z.copy()
+        p[idx] += h
+        m_[idx] -= h
+        fd[idx] = ((k.K_tens_raw(p, increments) * G).sum() - (k.K_tens_raw(m_, increments) * G).sum()) / (2 * h)
+    np.testing.assert_allclose(Zt.grad.numpy(), fd, rtol=1e-5, atol=1e-7)
