@@ -61,6 +61,9 @@ SIGNATURES = {
     "gpsig_rescaled": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _P, _P, _SZ, _P]),
     "gpsig_rescaled_workspace_bytes": (_SZ, [_I, _I]),
     "gpsig_tens_workspace_bytes": (_SZ, [_I, _I, _I, _I, _I]),
+    "gpsig_signature_channels": (ctypes.c_longlong, [_I, _I]),
+    "gpsig_signature": (_I, [_P, _I, _I, _I, _I, _P, _P]),
+    "gpsig_signature_vjp": (_I, [_P, _I, _I, _I, _I, _P, _P, _P]),
     "gpsig_version": (ctypes.c_char_p, []),
 }
 

@@ -168,3 +168,18 @@ class PdeGram(torch.autograd.Function):
         Xs, X2s = ctx.saved_tensors
         gX, gY = ops.pde_gram_vjp(Xs.detach(), None if X2s is None else X2s.detach(), gout, ctx.dyadic, ctx.solver)
         return (gX.to(Xs.dtype), None if gY is None else gY.to(X2s.dtype), None, None)
+
+
+class Signature(torch.autograd.Function):
+    """Truncated signatures (iisignature.sig) with the gfx950 backward (iisignature.sigbackprop)."""
+
+    @staticmethod
+    def forward(ctx, X, depth):
+        ctx.depth = depth
+        ctx.save_for_backward(X)
+        return ops.signature(X.detach(), depth)
+
+    @staticmethod
+    def backward(ctx, gout):
+        (X,) = ctx.saved_tensors
+        return ops.signature_vjp(X.detach(), ctx.depth, gout).to(X.dtype), None

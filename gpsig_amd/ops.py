@@ -245,6 +245,34 @@ def pde_gram_vjp(X: torch.Tensor, Y: torch.Tensor | None, gout: torch.Tensor, dy
     return gX, (None if sym else gY)
 
 
+# ----------------------------------------------------------------------------- signature features
+def signature(X: torch.Tensor, depth: int) -> torch.Tensor:
+    """Truncated signatures, levels 1..depth flattened first-index-major (iisignature.sig layout):
+    X (n, l, d) -> (n, sum_m d^m) float32."""
+    _require_cuda(X)
+    lib = L.load()
+    X = _f32(X)
+    n, l, d = X.shape
+    out = torch.empty((n, int(lib.gpsig_signature_channels(d, depth))), dtype=torch.float32, device=X.device)
+    L.check(lib.gpsig_signature(X.data_ptr(), n, l, d, depth, out.data_ptr(), _stream(X.device)), "gpsig_signature")
+    return out
+
+
+def signature_vjp(X: torch.Tensor, depth: int, gout: torch.Tensor, gX: torch.Tensor | None = None) -> torch.Tensor:
+    """dLoss/dX of signature() given gout (n, channels) (iisignature.sigbackprop)."""
+    _require_cuda(X, gout)
+    lib = L.load()
+    X, gout = _f32(X), _f32(gout)
+    n, l, d = X.shape
+    if tuple(gout.shape) != (n, int(lib.gpsig_signature_channels(d, depth))):
+        raise ValueError("gout must be (n, channels)")
+    if gX is None:
+        gX = torch.zeros((n, l, d), dtype=torch.float32, device=X.device)
+    L.check(lib.gpsig_signature_vjp(X.data_ptr(), n, l, d, depth, gout.data_ptr(), gX.data_ptr(), _stream(X.device)),
+            "gpsig_signature_vjp")
+    return gX
+
+
 # ----------------------------------------------------------------------------- multi-GPU helper
 def sym_assemble(src: torch.Tensor, row_off: torch.Tensor, level_stride: int, n: int, levels: int,
                  out: torch.Tensor | None = None) -> torch.Tensor:

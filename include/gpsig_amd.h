@@ -187,6 +187,21 @@ int gpsig_pde_vjp(const float *X, int n1, int l1, const float *Y, int n2, int l2
                   size_t workspace_bytes, gpsig_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
+ * Truncated signatures (replaces iisignature.sig behind iisignature_tensorflow.Sig,
+ * gpsig/iisignature_tensorflow.py:87, used by the VOSF Kuf, gpsig/inducing_variables_vosf.py:120-146).
+ * X (n, l, d) -> out (n, gpsig_signature_channels(d, depth)): levels 1..depth, each flattened
+ * first-index-major, concatenated (iisignature.sig's layout).  Needs (channels + d) * 4 <= 64 KiB.
+ */
+long long gpsig_signature_channels(int d, int depth);
+
+int gpsig_signature(const float *X, int n, int l, int d, int depth, float *out, gpsig_stream_t stream);
+
+/* Gradient of gpsig_signature (iisignature.sigbackprop behind the Sig op's gradient): gout (n, channels)
+ * = dLoss/dsig; accumulates (+=) gX (n, l, d).  Needs (3 channels + 2 d) * 4 <= 64 KiB. */
+int gpsig_signature_vjp(const float *X, int n, int l, int d, int depth, const float *gout, float *gX,
+                        gpsig_stream_t stream);
+
+/* ---------------------------------------------------------------------------------------------
  * Multi-GPU assembly helper (no reference counterpart: the reference has no distributed code).
  * After an all-gather of UPPER-mode row blocks, build the full symmetric matrix:
  *   dst[l][a][b] = src[row_off[a] + l*level_stride + b]   for b >= a,

@@ -155,3 +155,18 @@ def k_tens(Zs, num_levels, base="rbf", increments=False):
             k += 1
         K.append(R)
     return torch.stack(K, 0)
+
+
+def signature(x: torch.Tensor, depth: int) -> torch.Tensor:
+    """Truncated signature of one path x (L, D) (Chen's identity, oracle/chen.py's definition) as a
+    differentiable torch fp64 function: levels 1..depth flattened first-index-major, concatenated --
+    the object iisignature.sig returns (iisignature_tensorflow.py:87)."""
+    D = x.shape[1]
+    S = [torch.ones(1, dtype=x.dtype)] + [torch.zeros(D ** m, dtype=x.dtype) for m in range(1, depth + 1)]
+    for k in range(x.shape[0] - 1):
+        v = x[k + 1] - x[k]
+        E = [torch.ones(1, dtype=x.dtype)]
+        for m in range(1, depth + 1):
+            E.append(torch.outer(E[-1], v).reshape(-1) / m)
+        S = [sum(torch.outer(S[j], E[m - j]).reshape(-1) for j in range(m + 1)) for m in range(depth + 1)]
+    return torch.cat(S[1:])

@@ -1,0 +1,79 @@
+"""Signature features (iisignature.sig / sigbackprop replacement): host helpers on CPU, the gfx950
+kernels vs the Chen-identity oracle (oracle/chen.py, pinned to the esig relation in test_oracle.py)."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import norm_rel_err
+from oracle import autodiff_ref as ar
+from oracle import chen
+
+DEV = "cuda"
+
+
+def test_compute_trunc_and_powers():
+    from gpsig_amd import signatures as sg
+    assert sg.compute_trunc(6, 5) == 1 and sg.compute_trunc(7, 5) == 2 and sg.compute_trunc(100, 5) == 3
+    P = sg.get_powers(3, 2)
+    assert P.shape == (3 + 9, 3)
+    np.testing.assert_array_equal(P[3], [2, 0, 0])  # (1,1)
+    np.testing.assert_array_equal(P[4], [1, 1, 0])  # (1,2)
+    np.testing.assert_array_equal(P[3 + 5], [0, 1, 1])  # (2,3)
+    np.testing.assert_array_equal(P.sum(1), [1] * 3 + [2] * 9)
+
+
+def test_torch_signature_oracle_matches_chen():
+    rng = np.random.default_rng(0)
+    x = np.cumsum(rng.standard_normal((7, 3)), 0) * 0.3
+    ref = np.concatenate(chen.signature(x, 4)[1:])
+    np.testing.assert_allclose(ar.signature(torch.tensor(x), 4).numpy(), ref, rtol=1e-12, atol=1e-14)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d,depth,L", [(2, 6, 30), (3, 4, 50), (5, 5, 40), (1, 3, 10), (8, 3, 20)])
+def test_signature_matches_chen(d, depth, L):
+    from gpsig_amd import ops
+    rng = np.random.default_rng(d + depth)
+    X = np.cumsum(rng.standard_normal((9, L, d)), 1) / np.sqrt(L)
+    got = ops.signature(torch.tensor(X, device=DEV), depth).cpu().numpy()
+    off = 0
+    for m in range(1, depth + 1):
+        ref = np.stack([chen.signature(x, depth)[m] for x in X])
+        assert norm_rel_err(got[:, off:off + d ** m], ref) < 1e-5, m
+        off += d ** m
+    assert off == got.shape[1]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("d,depth,L", [(2, 4, 12), (3, 3, 20), (5, 3, 15)])
+def test_signature_backprop_matches_autodiff(d, depth, L):
+    from gpsig_amd import signatures as sg
+    rng = np.random.default_rng(10 + d)
+    X = np.cumsum(rng.standard_normal((5, L, d)), 1) / np.sqrt(L)
+    C = sum(d ** m for m in range(1, depth + 1))
+    G = rng.standard_normal((5, C))
+    Xt = torch.tensor(X, device=DEV, requires_grad=True)
+    (sg.Sig(Xt, depth) * torch.as_tensor(G, device=DEV)).sum().backward()
+    ref = np.zeros_like(X)
+    for a in range(5):
+        xa = torch.tensor(X[a], requires_grad=True)
+        (ar.signature(xa, depth) * torch.tensor(G[a])).sum().backward()
+        ref[a] = xa.grad.numpy()
+    assert norm_rel_err(Xt.grad.cpu().numpy(), ref) < 5e-5
+
+
+@pytest.mark.gpu
+def test_vosf_kuf_shape_and_values():
+    import gpsig_amd
+    from gpsig_amd import signatures as sg
+    rng = np.random.default_rng(3)
+    N, L, d, M = 6, 20, 3, 10
+    X = np.cumsum(rng.standard_normal((N, L, d)), 1) / np.sqrt(L)
+    k = gpsig_amd.UntruncSignatureKernel(L * d, d, lengthscales=np.array([0.5, 1.0, 2.0]))
+    Kuf = sg.vosf_Kuf(k, torch.tensor(X.reshape(N, -1), device=DEV), M, d).cpu().numpy()
+    assert Kuf.shape == (M, N)
+    lvl = sg.compute_trunc(M, d)
+    S = np.stack([np.concatenate(chen.signature(x, lvl)[1:]) for x in X])[:, :M - 1]
+    S = S / np.prod(np.array([0.5, 1.0, 2.0])[None, :] ** sg.get_powers(d, lvl)[:M - 1], axis=1)[None, :]
+    np.testing.assert_allclose(Kuf[0], 1.0)
+    assert norm_rel_err(Kuf[1:].T, S) < 1e-5
