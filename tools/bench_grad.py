@@ -1,8 +1,10 @@
 #!/usr/bin/env python
-"""Forward and forward+backward time of the normalised K(X) (SignatureRBF, order 1) on one GPU, and the
-gradient's error vs torch fp64 autodiff of the reference graph (oracle/autodiff_ref.py) on a subsample.
+"""Forward vs forward+backward time of the differentiable paths on one GPU (median of --reps
+device-synchronised calls, inputs resident), with the gradient's error vs torch fp64 autodiff of the
+reference graph (oracle/autodiff_ref.py) / the reference's PDE adjoint (oracle/pde_grad.py) on a
+subsample.  One JSON object per line.
 
-    python tools/bench_grad.py --n 1024 --l 100 --d 5 --m 5
+    python tools/bench_grad.py [--only gram,kuf,pde,sig]
 """
 import argparse
 import json
@@ -18,56 +20,152 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--n", type=int, default=1024)
-    ap.add_argument("--l", type=int, default=100)
-    ap.add_argument("--d", type=int, default=5)
-    ap.add_argument("--m", type=int, default=5)
-    ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--check", type=int, default=8, help="sequences in the fp64 autodiff check (0 = skip)")
-    a = ap.parse_args()
+def walks(n, l, d, seed):
+    rng = np.random.default_rng(seed)
+    return np.cumsum(rng.standard_normal((n, l, d)), axis=1) / np.sqrt(l * d)
+
+
+def timed(fn, reps):
+    fn()
+    torch.cuda.synchronize()
+    ts = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        fn()
+        torch.cuda.synchronize()
+        ts.append(time.perf_counter() - t0)
+    return statistics.median(ts)
+
+
+def rel(g, r):
+    return float(np.abs(g - r).max() / np.abs(r).max())
+
+
+def bench_gram(reps, n=1024, l=100, d=5, m=5):
     import gpsig_amd
     from oracle import autodiff_ref as ar
-    rng = np.random.default_rng(0)
-    Xnp = np.cumsum(rng.standard_normal((a.n, a.l, a.d)), axis=1) / np.sqrt(a.l * a.d)
-    X = torch.tensor(Xnp.reshape(a.n, -1), device="cuda", dtype=torch.float32)
-    G = torch.randn(a.n, a.n, device="cuda")
-    k = gpsig_amd.SignatureRBF(a.l * a.d, a.d, a.m)
+    Xnp = walks(n, l, d, 0)
+    X = torch.tensor(Xnp.reshape(n, -1), device="cuda", dtype=torch.float32)
+    G = torch.randn(n, n, device="cuda")
+    k = gpsig_amd.SignatureRBF(l * d, d, m)
 
     def fwd():
         with torch.no_grad():
-            return k.K(X)
+            k.K(X)
 
-    def fwdbwd():
+    def fb():
         Xg = X.detach().requires_grad_(True)
         (k.K(Xg) * G).sum().backward()
-        return Xg.grad
 
-    def timed(fn):
-        fn()
-        torch.cuda.synchronize()
-        ts = []
-        for _ in range(a.reps):
-            t0 = time.perf_counter()
-            fn()
-            torch.cuda.synchronize()
-            ts.append(time.perf_counter() - t0)
-        return statistics.median(ts)
+    tf, tb = timed(fwd, reps), timed(fb, reps)
+    S = 8
+    Xs = torch.tensor(Xnp[:S].reshape(S, -1), device="cuda", requires_grad=True)
+    Gs = torch.randn(S, S, dtype=torch.float64)
+    (k.K(Xs) * Gs.to("cuda")).sum().backward()
+    Xr = torch.tensor(Xnp[:S], requires_grad=True)
+    (ar.K(Xr, None, m) * Gs).sum().backward()
+    return dict(path="gram", workload=f"SignatureRBF K(X) normalised N={n} L={l} D={d} M={m}", fwd_ms=tf * 1e3,
+                fwd_bwd_ms=tb * 1e3, grad_err=rel(Xs.grad.reshape(Xr.shape).cpu().numpy(), Xr.grad.numpy()))
 
-    tf, tb = timed(fwd), timed(fwdbwd)
-    res = dict(workload=f"SignatureRBF K(X) normalised N={a.n} L={a.l} D={a.d} M={a.m}", fwd_ms=tf * 1e3,
-               fwd_bwd_ms=tb * 1e3, bwd_over_fwd=(tb - tf) / tf, entries_per_s_fwd_bwd=a.n * a.n / tb)
-    if a.check:
-        S = a.check
-        Xs = torch.tensor(Xnp[:S].reshape(S, -1), device="cuda", requires_grad=True)
-        Gs = torch.randn(S, S, dtype=torch.float64)
-        (k.K(Xs) * Gs.to("cuda")).sum().backward()
-        Xr = torch.tensor(Xnp[:S], requires_grad=True)
-        (ar.K(Xr, None, a.m) * Gs).sum().backward()
-        g, r = Xs.grad.reshape(Xr.shape).cpu().numpy(), Xr.grad.numpy()
-        res["grad_norm_rel_err"] = float(np.abs(g - r).max() / np.abs(r).max())
-    print(json.dumps(res))
+
+def bench_kuf(reps, t=512, n=1024, l=100, d=5, m=5, increments=False):
+    import gpsig_amd
+    from oracle import autodiff_ref as ar
+    lt = m * (m + 1) // 2
+    rng = np.random.default_rng(2)
+    Znp = rng.standard_normal((lt, t, 2, d) if increments else (lt, t, d))
+    Xnp = walks(n, l, d, 0)
+    Z = torch.tensor(Znp, device="cuda", dtype=torch.float32)
+    X = torch.tensor(Xnp.reshape(n, -1), device="cuda", dtype=torch.float32)
+    G = torch.randn(t, n, device="cuda")
+    k = gpsig_amd.SignatureRBF(l * d, d, m)
+
+    def fwd():
+        with torch.no_grad():
+            k.K_tens_vs_seq(Z, X, increments=increments)
+
+    def fb():
+        Zg = Z.detach().requires_grad_(True)
+        (k.K_tens_vs_seq(Zg, X, increments=increments) * G).sum().backward()
+
+    tf, tb = timed(fwd, reps), timed(fb, reps)
+    S, TS = 6, 5
+    Zs = torch.tensor(Znp[:, :TS], device="cuda", requires_grad=True)
+    Gs = torch.randn(TS, S, dtype=torch.float64)
+    (k.K_tens_vs_seq(Zs, torch.tensor(Xnp[:S].reshape(S, -1), device="cuda"), increments=increments)
+     * Gs.to("cuda")).sum().backward()
+    Zr = torch.tensor(Znp[:, :TS], requires_grad=True)
+    (ar.K_tens_vs_seq(Zr, torch.tensor(Xnp[:S]), m, increments=increments) * Gs).sum().backward()
+    return dict(path="kuf" + ("_incr" if increments else ""),
+                workload=f"K_tens_vs_seq normalised T={t} N={n} L={l} D={d} M={m} increments={increments} (dZ)",
+                fwd_ms=tf * 1e3, fwd_bwd_ms=tb * 1e3, grad_err=rel(Zs.grad.cpu().numpy(), Zr.grad.numpy()))
+
+
+def bench_pde(reps, n=1024, l=200, d=5, dyadic=1):
+    import gpsig_amd
+    from oracle import pde, pde_grad
+    Xnp = walks(n, l, d, 0)
+    X = torch.tensor(Xnp.reshape(n, -1), device="cuda", dtype=torch.float32)
+    w = torch.randn(n, device="cuda")
+    k = gpsig_amd.UntruncSignatureKernel(l * d, d, order=dyadic)
+
+    def fwd():
+        with torch.no_grad():
+            k.Kdiag(X)
+
+    def fb():
+        Xg = X.detach().requires_grad_(True)
+        (k.Kdiag(Xg) * w).sum().backward()
+
+    tf, tb = timed(fwd, reps), timed(fb, reps)
+    S = 4
+    Xs = torch.tensor(Xnp[:S].reshape(S, -1), device="cuda", requires_grad=True)
+    k.Kdiag(Xs).sum().backward()
+    K, Kr = pde.pde_diag_grids(Xnp[:S], dyadic, 1)
+    ref = pde_grad.kdiag_grad(Xnp[:S], np.tril(K), np.tril(Kr), dyadic)
+    return dict(path="pde_kdiag", workload=f"UntruncSignatureKernel Kdiag N={n} L={l} D={d} dyadic={dyadic}",
+                fwd_ms=tf * 1e3, fwd_bwd_ms=tb * 1e3, grad_err=rel(Xs.grad.reshape(ref.shape).cpu().numpy(), ref))
+
+
+def bench_sig(reps, n=4096, l=100, d=5, depth=3):
+    from gpsig_amd import signatures as sg
+    from oracle import autodiff_ref as ar
+    Xnp = walks(n, l, d, 0)
+    X = torch.tensor(Xnp, device="cuda", dtype=torch.float32)
+    C = sum(d ** m for m in range(1, depth + 1))
+    G = torch.randn(n, C, device="cuda")
+
+    def fwd():
+        with torch.no_grad():
+            sg.Sig(X, depth)
+
+    def fb():
+        Xg = X.detach().requires_grad_(True)
+        (sg.Sig(Xg, depth) * G).sum().backward()
+
+    tf, tb = timed(fwd, reps), timed(fb, reps)
+    xs = torch.tensor(Xnp[0], requires_grad=True)
+    Xg = torch.tensor(Xnp[:1], device="cuda", requires_grad=True)
+    g0 = torch.randn(C, dtype=torch.float64)
+    (sg.Sig(Xg, depth) * g0.to("cuda")[None]).sum().backward()
+    (ar.signature(xs, depth) * g0).sum().backward()
+    return dict(path="signature", workload=f"Sig N={n} L={l} d={d} depth={depth}", fwd_ms=tf * 1e3,
+                fwd_bwd_ms=tb * 1e3, grad_err=rel(Xg.grad[0].cpu().numpy(), xs.grad.numpy()))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--only", default="gram,kuf,kuf_incr,pde,sig")
+    a = ap.parse_args()
+    todo = a.only.split(",")
+    runs = dict(gram=lambda: bench_gram(a.reps), kuf=lambda: bench_kuf(a.reps),
+                kuf_incr=lambda: bench_kuf(a.reps, increments=True), pde=lambda: bench_pde(a.reps),
+                sig=lambda: bench_sig(a.reps))
+    for name in todo:
+        r = runs[name]()
+        r["bwd_over_fwd"] = (r["fwd_bwd_ms"] - r["fwd_ms"]) / r["fwd_ms"]
+        print(json.dumps(r), flush=True)
 
 
 if __name__ == "__main__":
