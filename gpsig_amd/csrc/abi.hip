@@ -5,7 +5,7 @@
 namespace gpsig {
 int features(const float *X, int n, int l, int d, int DP, float *F, hipStream_t s);
 int sig_fo_launch(const SigArgs &a, int DP, int seed, long long nblocks, hipStream_t s);
-int fo_lanes_per_pair(int l2, int DP);
+int fo_lanes_per_pair(int l2, int DP, int M);
 int sig_ho_launch(const SigArgs &a, int DP, int seed, long long nblocks, hipStream_t s);
 int ho_lanes_per_pair(int l2, int order, int M);
 int pde_launch(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int dyadic, int solver,
@@ -97,7 +97,7 @@ extern "C" int gpsig_sig_gram(const float *X, int n1, int l1, const float *Y, in
   a.out_ld = n2;
   a.out_lvl = (long long)out_rows * n2;
 
-  const int LP = (order == 1) ? fo_lanes_per_pair(l2, DP) : ho_lanes_per_pair(l2, order, num_levels);
+  const int LP = (order == 1) ? fo_lanes_per_pair(l2, DP, num_levels) : ho_lanes_per_pair(l2, order, num_levels);
   if (LP == 0) return GPSIG_EUNSUPPORTED;
   const int G = 64 / LP;
   long long nblocks = 0;

@@ -168,15 +168,21 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
 // The lane keeps 2*W*DP column floats (y, dy) in VGPRs, so wide channel counts take fewer columns per
 // lane (more lanes per pair): W*DP <= 64 keeps the kernel within 256 VGPRs.
 struct Geo { int W, LP; };
-__host__ __device__ constexpr int fo_wmax(int DP) { return DP <= 8 ? 8 : (DP <= 16 ? 4 : 2); }
+// W = 8 only while the kernel stays within 256 VGPRs (no AGPR spill): measured on MI355X with
+// tools/kbench.hip, W = 8 / LP = 16 beats W = 4 / LP = 32 by 8-18 % when it fits (D <= 5, any M;
+// D = 6, M <= 5) and loses 30-50 % when it does not (D = 6, M = 7: 49.4 vs 37.8 ms; D = 8, M = 6:
+// 220 vs 149 ms at N = 4096).
+__host__ __device__ constexpr int fo_wmax(int DP, int M) {
+  return DP <= 5 ? 8 : (DP <= 6 ? (M <= 5 ? 8 : 4) : (DP <= 16 ? 4 : 2));
+}
 // longest sequences: W may exceed fo_wmax at LP = 64 (register spills, still correct)
 __host__ __device__ constexpr int fo_wcap(int DP) { return DP <= 16 ? 8 : 4; }
-inline Geo fo_geometry(int l2, int DP) {
+inline Geo fo_geometry(int l2, int DP, int M) {
   // smallest LP (shortest scans) at which some W <= fo_wmax covers the sequence, smallest such W
   for (int LP : {16, 32, 64})
-    for (int W = 2; W <= fo_wmax(DP); W *= 2)
+    for (int W = 2; W <= fo_wmax(DP, M); W *= 2)
       if (LP * W >= l2) return {W, LP};
-  for (int W = 2 * fo_wmax(DP); W <= fo_wcap(DP); W *= 2)
+  for (int W = 2 * fo_wmax(DP, M); W <= fo_wcap(DP); W *= 2)
     if (64 * W >= l2) return {W, 64};
   return {0, 0};
 }
@@ -194,8 +200,8 @@ int launch_fo(const SigArgs &a, long long nblocks, hipStream_t s) {
 
 template <int DP, int M, int SEED>
 int fo_geo(const SigArgs &a, long long nblocks, hipStream_t s) {
-  const Geo geo = fo_geometry(a.l2, DP);
-  constexpr int WM = fo_wmax(DP), WC = fo_wcap(DP);
+  const Geo geo = fo_geometry(a.l2, DP, M);
+  constexpr int WM = fo_wmax(DP, M), WC = fo_wcap(DP);
 #define GPSIG_GEO(w, lp) \
   if (geo.W == w && geo.LP == lp) return launch_fo<DP, w, lp, M, SEED>(a, nblocks, s);
   GPSIG_GEO(2, 16) GPSIG_GEO(2, 32) GPSIG_GEO(2, 64)

@@ -63,17 +63,60 @@ def test_signature_backprop_matches_autodiff(d, depth, L):
 
 
 @pytest.mark.gpu
-def test_vosf_kuf_shape_and_values():
+def test_vosf_untrunc_features():
+    """UntruncInducingOrthogonalTensors.Kuu_Kuf_Kff (inducing_variables_vosf.py:68-146)."""
     import gpsig_amd
+    from gpsig_amd import inducing_variables_vosf as iv
     from gpsig_amd import signatures as sg
+    from oracle import pde
     rng = np.random.default_rng(3)
     N, L, d, M = 6, 20, 3, 10
     X = np.cumsum(rng.standard_normal((N, L, d)), 1) / np.sqrt(L)
-    k = gpsig_amd.UntruncSignatureKernel(L * d, d, lengthscales=np.array([0.5, 1.0, 2.0]))
-    Kuf = sg.vosf_Kuf(k, torch.tensor(X.reshape(N, -1), device=DEV), M, d).cpu().numpy()
-    assert Kuf.shape == (M, N)
+    ls = np.array([0.5, 1.0, 2.0])
+    k = gpsig_amd.UntruncSignatureKernel(L * d, d, lengthscales=ls, order=1)
+    feat = iv.UntruncInducingOrthogonalTensors(L * d, d, M, compute_sig=True)
+    Kzz, Kzx, Kxx = iv.Kuu_Kuf_Kff(feat, k, torch.tensor(X.reshape(N, -1), device=DEV))
     lvl = sg.compute_trunc(M, d)
     S = np.stack([np.concatenate(chen.signature(x, lvl)[1:]) for x in X])[:, :M - 1]
-    S = S / np.prod(np.array([0.5, 1.0, 2.0])[None, :] ** sg.get_powers(d, lvl)[:M - 1], axis=1)[None, :]
-    np.testing.assert_allclose(Kuf[0], 1.0)
-    assert norm_rel_err(Kuf[1:].T, S) < 1e-5
+    S = S / np.prod(ls[None, :] ** sg.get_powers(d, lvl)[:M - 1], axis=1)[None, :]
+    np.testing.assert_allclose(Kzz.cpu().numpy(), np.eye(M))
+    assert Kzx.shape == (M, N)
+    np.testing.assert_allclose(Kzx[0].cpu().numpy(), 1.0)
+    assert norm_rel_err(Kzx[1:].T.cpu().numpy(), S) < 1e-5
+    assert norm_rel_err(Kxx.cpu().numpy(), pde.pde_diag(X / ls, 1, 1)) < 1e-5
+    # compute_and_diff_sig: signatures of the scaled paths, differentiable in the lengthscales
+    feat2 = iv.UntruncInducingOrthogonalTensors(L * d, d, M, compute_and_diff_sig=True)
+    k.lengthscales = torch.tensor(ls, device=DEV, requires_grad=True)
+    Kzx2 = feat2.Kuf(k, torch.tensor(X.reshape(N, -1), device=DEV))
+    assert norm_rel_err(Kzx2[1:].T.detach().cpu().numpy(), S) < 1e-5  # same numbers, other route
+    Kzx2.sum().backward()
+    assert torch.isfinite(k.lengthscales.grad).all()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("normalization", [True, False])
+def test_vosf_trunc_features(normalization):
+    """TruncInducingOrthogonalTensors.Kuu_Kuf_Kff (inducing_variables_vosf.py:180-269)."""
+    import gpsig_amd
+    from gpsig_amd import inducing_variables_vosf as iv
+    from gpsig_amd import signatures as sg
+    from oracle import kernels_ref as kr
+    rng = np.random.default_rng(4)
+    N, L, d, M, lev = 5, 16, 2, 9, 4
+    X = np.cumsum(rng.standard_normal((N, L, d)), 1) / np.sqrt(L)
+    var = np.array([1.0, 0.5, 2.0, 1.5, 0.7])
+    k = gpsig_amd.SignatureLinear(L * d, d, lev, variances=var, normalization=normalization)
+    feat = iv.TruncInducingOrthogonalTensors(L * d, d, M, compute_sig=True)
+    Kzz, Kzx, Kxx = feat.Kuu_Kuf_Kff(k, torch.tensor(X.reshape(N, -1), device=DEV))
+    slv = sg.compute_trunc(M, d)
+    S = np.stack([np.concatenate([[1.0]] + chen.signature(x, slv)[1:]) for x in X])[:, :M].T  # (M, N)
+    reps = np.repeat(np.arange(slv + 1), [d ** i for i in range(slv + 1)])[:M]
+    S = S * np.sqrt(var[reps])[:, None]
+    ref = kr.SignatureKernelRef(L * d, d, lev, base="linear", variances=var, normalization=normalization)
+    if normalization:
+        Kun = ref.K_seq_diag(X)
+        S = S / np.sqrt(Kun[reps] + 1e-6)
+        np.testing.assert_allclose(Kxx.cpu().numpy(), var.sum())
+    else:
+        assert norm_rel_err(Kxx.cpu().numpy(), ref.Kdiag(X.reshape(N, -1))) < 1e-5
+    assert norm_rel_err(Kzx.cpu().numpy(), S) < 1e-5
