@@ -45,10 +45,18 @@ __device__ __forceinline__ void tvs_bwd_level(const TvsBwdArgs &a) {
   const bool valid = s0 < n;
   const int sq = valid ? s0 : n - 1;
   const int zs = INCR ? 2 * d : d;
-  const float *__restrict__ Z = a.Z;
+  // the level's components of this tensor (wave-uniform), staged in LDS: broadcast reads instead of
+  // the serialised L2-latency vector loads the compiler emits for uniform global data it cannot prove
+  // invariant
+  __shared__ float zl[I * 2 * DP];
+  for (int e = lane; e < I * 2 * DP; e += 64) {
+    const int c = e / (2 * DP), h = (e / DP) % 2, q = e % DP;
+    zl[e] = (q < d && (INCR || h == 0)) ? a.Z[((long long)(KB + c) * T + tt) * zs + h * d + q] : 0.f;
+  }
+  __syncthreads();
   // component c of the level (global component KB + c)
-  auto z0c = [&](int c, int q) -> float { return q < d ? Z[((long long)(KB + c) * T + tt) * zs + q] : 0.f; };
-  auto z1c = [&](int c, int q) -> float { return q < d ? Z[((long long)(KB + c) * T + tt) * zs + d + q] : 0.f; };
+  auto z0c = [&](int c, int q) -> float { return zl[(c * 2) * DP + q]; };
+  auto z1c = [&](int c, int q) -> float { return zl[(c * 2 + 1) * DP + q]; };
   auto ld = [&](int s, int c) -> float { return a.Ft[((long long)s * FC + c) * n + sq]; };
   auto ldx = [&](int s, float (&x)[DP]) {
 #pragma unroll

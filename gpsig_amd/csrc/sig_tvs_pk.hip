@@ -54,7 +54,13 @@ __global__ __launch_bounds__(256) void tvs_prep_kernel(const float *__restrict__
 }
 
 template <int DP, int M, bool INCR>
-__global__ __launch_bounds__(64) void tvs_pk_kernel(TvsPkArgs a) {
+#ifndef GPSIG_TVS_WPE
+#define GPSIG_TVS_WPE 2
+#endif
+#ifndef GPSIG_TVS_WPE0
+#define GPSIG_TVS_WPE0 1
+#endif
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(INCR ? GPSIG_TVS_WPE : GPSIG_TVS_WPE0))) void tvs_pk_kernel(TvsPkArgs a) {
   constexpr int LT = M * (M + 1) / 2;
   constexpr int ZS = tvs_zs<DP, INCR>();
   constexpr int ANCHOR = 8;
@@ -62,10 +68,18 @@ __global__ __launch_bounds__(64) void tvs_pk_kernel(TvsPkArgs a) {
   constexpr float NHL2E = -0.72134752044448170f, L2E = 1.4426950408889634f;
   const int lane = threadIdx.x;
   const int tt = blockIdx.y;
-  const int n = a.n, d = a.d, FC = 2 * d + 3;
+  // instantiated per exact channel count (DP == a.d): no per-channel guards in the time loop
+  constexpr int d = DP;
+  const int n = a.n, FC = 2 * d + 3;
   const int s0 = blockIdx.x * 128 + lane, s1 = s0 + 64;
   const int c0 = s0 < n ? s0 : n - 1, c1 = s1 < n ? s1 : n - 1;
-  const float *__restrict__ zp = a.Zp + (long long)tt * LT * ZS;
+  // The tensor's components are wave-uniform: staged once in LDS (broadcast reads, ~100-cycle
+  // latency) instead of the L2-latency global loads the compiler emits for them (it cannot prove the
+  // prepared buffer invariant against the output stores, so it does not use scalar loads).
+  __shared__ __attribute__((aligned(16))) float zl[LT * ZS];
+  for (int e = lane; e < LT * ZS; e += 64) zl[e] = a.Zp[(long long)tt * LT * ZS + e];
+  __syncthreads();
+  const float *zp = zl;
 
   // loads of channel c of cell s for both sequences of the lane
   auto ld = [&](int s, int c) {
@@ -112,7 +126,7 @@ __global__ __launch_bounds__(64) void tvs_pk_kernel(TvsPkArgs a) {
 
   const int ncell = a.l - 1;
   for (int s = 0; s < ncell; ++s) {
-    // keeps the component loads inside the loop (hoisted, LT x ZS of them would not fit in SGPRs)
+    // keeps the component reads inside the loop (hoisted, LT x ZS of them would not fit in registers)
     asm volatile("" ::: "memory");
     f2 dx[DP];
 #pragma unroll
@@ -130,6 +144,9 @@ __global__ __launch_bounds__(64) void tvs_pk_kernel(TvsPkArgs a) {
 #pragma unroll
       for (int st = 0; st < i; ++st) {
         const int k = k0 + st;
+        // one component's LDS reads at a time: scheduled all up front they would keep LT x ZS values
+        // live (the increments kernel then spilled to AGPRs)
+        if constexpr (INCR) asm volatile("" ::: "memory");
         const float *z = zp + k * ZS;
         f2 qv = -g, cv = splat2(0.f);
 #pragma unroll
@@ -240,13 +257,13 @@ static int tvs_pk_m(int M, const float *Z, int lt, int t, int d, const float *Ft
 int tvs_pk_launch(const float *Z, int lt, int t, int increments, int d, const float *Ft, int n, int l, int M,
                   float *out, float *Zp, hipStream_t s) {
   if (M > 6 || d > 8 || l < 2) return -1;
-  const int DP = d <= 2 ? 2 : d <= 4 ? 4 : d <= 6 ? 6 : 8;
+  const int DP = d;
 #define GPSIG_TVS(dp)                                                               \
   case dp:                                                                          \
     return increments ? tvs_pk_m<dp, true>(M, Z, lt, t, d, Ft, n, l, out, Zp, s)    \
                       : tvs_pk_m<dp, false>(M, Z, lt, t, d, Ft, n, l, out, Zp, s);
   switch (DP) {
-    GPSIG_TVS(2) GPSIG_TVS(4) GPSIG_TVS(6) GPSIG_TVS(8)
+    GPSIG_TVS(1) GPSIG_TVS(2) GPSIG_TVS(3) GPSIG_TVS(4) GPSIG_TVS(5) GPSIG_TVS(6) GPSIG_TVS(7) GPSIG_TVS(8)
     default: return -1;
   }
 #undef GPSIG_TVS
