@@ -248,77 +248,56 @@ class SignatureKernel:
         Kzx = Kzx * (self.sigma * self.variances).to(Xs.device, torch.float32)[:, None, None]
         return (Kzx if return_levels else Kzx.sum(0)).to(dt)
 
+    def _sv(self, device):
+        """sigma * variances as float32 on device, differentiable in variances."""
+        return (self.sigma * self.variances).to(device, torch.float32)
+
+    def _gram_levels(self, Xs, X2s=None):
+        """Normalised (if self.normalization) per-level K(X[, X2]) x sigma*variances, differentiable."""
+        return _ag.SigGram.apply(Xs, X2s, (self.sigma * self.variances).to(Xs.device), self._cfg(True))
+
     def K_tens_n_seq_covs(self, Z, X, full_X_cov=False, return_levels=False, increments=False, presliced=False):
-        """kernels.py:624-704."""
+        """kernels.py:624-704 (differentiable in Z, X, lengthscales, variances)."""
         Zt = _as_tensor(Z)
         dt = self._out_dtype(X)
         Xs = self._prep(X, presliced)
         N = Xs.shape[0]
         Zs = self._apply_scaling_to_incremental_tensors(Zt) if increments else self._apply_scaling_to_tensors(Zt)
-        sv = self._scale_vec(Xs.device)
+        sv = self._sv(Xs.device)
         Kzz = self._K_tens(Zs, increments) * sv[:, None, None]
         Kzx = self._K_tens_vs_seq(Zs, Xs, increments)
+        if self.normalization:
+            Kzx = Kzx * self._rs_diff(Xs)[:, None, :]
+        Kzx = Kzx * sv[:, None, None]
         if full_X_cov:
-            if self.normalization:
-                rs = self._rsqrt_diag(Xs)
-                Kxx = ops.sig_gram(Xs, None, self.num_levels, self.order, self.base, self.difference, rs1=rs, rs2=rs,
-                                   scale=sv, jitter=self.jitter, out_mode=L.OUT_NORM_LEVELS)
-                Kzx = Kzx * rs[:, None, :]
-            else:
-                Kxx = ops.sig_gram(Xs, None, self.num_levels, self.order, self.base, self.difference, scale=sv,
-                                   out_mode=L.OUT_NORM_LEVELS)
-            Kzx = Kzx * sv[:, None, None]
-            out = (Kzz, Kzx, Kxx)
+            Kxx = self._gram_levels(Xs)
+        elif self.normalization:
+            Kxx = sv[:, None].repeat(1, N)
         else:
-            if self.normalization:
-                Kzx = Kzx * self._rsqrt_diag(Xs)[:, None, :]
-                Kxx = sv[:, None].repeat(1, N)
-            else:
-                Kxx = self._K_seq_diag(Xs) * sv[:, None]
-            Kzx = Kzx * sv[:, None, None]
-            out = (Kzz, Kzx, Kxx)
+            Kxx = self._K_seq_diag(Xs) * sv[:, None]
+        out = (Kzz, Kzx, Kxx)
         if not return_levels:
             out = tuple(o.sum(0) for o in out)
         return tuple(o.to(dt) for o in out)
 
     def K_seq_n_seq_covs(self, X, X2, full_X2_cov=False, return_levels=False, presliced=False):
-        """kernels.py:707-794 (the NameError branch at :756-761 restated with the intended names)."""
+        """kernels.py:707-794 (differentiable).  Two reference defects are not reproduced: the
+        NameError branch at :756-761 is restated with the intended names, and in the diagonal branch
+        Kxx2 is normalised once by each side's norms (:768 and :784 divide it by X's norms twice)."""
         dt = self._out_dtype(X)
         Xs = self._prep(X, True)  # reference slices only X2 here (kernels.py:712-713)
         X2s = self._prep(X2, presliced)
         N2 = X2s.shape[0]
-        sv = self._scale_vec(Xs.device)
-        if self.normalization:
-            rs = self._rsqrt_diag(Xs)
-            Kxx = ops.sig_gram(Xs, None, self.num_levels, self.order, self.base, self.difference, rs1=rs, rs2=rs,
-                               scale=sv, jitter=self.jitter, out_mode=L.OUT_NORM_LEVELS)
-        else:
-            Kxx = ops.sig_gram(Xs, None, self.num_levels, self.order, self.base, self.difference, scale=sv,
-                               out_mode=L.OUT_NORM_LEVELS)
+        sv = self._sv(Xs.device)
+        Kxx = self._gram_levels(Xs)
+        Kxx2 = self._gram_levels(Xs, X2s)
         if full_X2_cov:
-            if self.normalization:
-                rs2 = self._rsqrt_diag(X2s)
-                Kxx2 = ops.sig_gram(Xs, X2s, self.num_levels, self.order, self.base, self.difference, rs1=rs,
-                                    rs2=rs2, scale=sv, out_mode=L.OUT_NORM_LEVELS)
-                Kx2x2 = ops.sig_gram(X2s, None, self.num_levels, self.order, self.base, self.difference, rs1=rs2,
-                                     rs2=rs2, scale=sv, jitter=self.jitter, out_mode=L.OUT_NORM_LEVELS)
-            else:
-                Kxx2 = ops.sig_gram(Xs, X2s, self.num_levels, self.order, self.base, self.difference, scale=sv,
-                                    out_mode=L.OUT_NORM_LEVELS)
-                Kx2x2 = ops.sig_gram(X2s, None, self.num_levels, self.order, self.base, self.difference, scale=sv,
-                                     out_mode=L.OUT_NORM_LEVELS)
-            out = (Kxx, Kxx2, Kx2x2)
+            Kd = self._gram_levels(X2s)
+        elif self.normalization:
+            Kd = sv[:, None].repeat(1, N2)
         else:
-            if self.normalization:
-                rs2 = self._rsqrt_diag(X2s)
-                Kxx2 = ops.sig_gram(Xs, X2s, self.num_levels, self.order, self.base, self.difference, rs1=rs,
-                                    rs2=rs2, scale=sv, out_mode=L.OUT_NORM_LEVELS)
-                Kd = sv[:, None].repeat(1, N2)
-            else:
-                Kxx2 = ops.sig_gram(Xs, X2s, self.num_levels, self.order, self.base, self.difference, scale=sv,
-                                    out_mode=L.OUT_NORM_LEVELS)
-                Kd = self._K_seq_diag(X2s) * sv[:, None]
-            out = (Kxx, Kxx2, Kd)
+            Kd = self._K_seq_diag(X2s) * sv[:, None]
+        out = (Kxx, Kxx2, Kd)
         if not return_levels:
             out = tuple(o.sum(0) for o in out)
         return tuple(o.to(dt) for o in out)

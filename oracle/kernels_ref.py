@@ -24,7 +24,9 @@ here (``jitter=1e-6``).
 
 Known reference defects are NOT reproduced: the
 ``K_x2x2_lvls`` NameError branch of K_seq_n_seq_covs (kernels.py:756-761) is
-restated with the evidently intended names.
+restated with the evidently intended names, and its diagonal branch normalises
+Kxx2 once by each side's norms (kernels.py:768 and :784 both divide it by the
+norms of X, i.e. twice).
 """
 from __future__ import annotations
 

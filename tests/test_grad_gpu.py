@@ -206,3 +206,32 @@ def test_tens_gram_vjp_matches_autodiff(base, increments):
     assert norm_rel_err(K.detach().cpu().numpy(), Kr.detach().numpy()) < 1e-5
     assert norm_rel_err(Zt.grad.cpu().numpy(), Zr.grad.numpy()) < GTOL
     assert norm_rel_err(k.lengthscales.grad.cpu().numpy(), lr.grad.numpy()) < GTOL
+
+
+def test_K_tens_n_seq_covs_gradient():
+    """Gradient of a loss over all three outputs (Kzz, Kzx, full Kxx) of K_tens_n_seq_covs
+    (kernels.py:624-704), the SVGP covariance bundle, in Z, X and the variances."""
+    import gpsig_amd
+    M, T, N, L, D = 3, 5, 6, 15, 2
+    LT = M * (M + 1) // 2
+    rng = np.random.default_rng(40)
+    Z = 0.5 * rng.standard_normal((LT, T, D))
+    X = walks(N, L, D, 41)
+    G1, G2, G3 = rng.standard_normal((T, T)), rng.standard_normal((T, N)), rng.standard_normal((N, N))
+    var = np.linspace(0.5, 1.5, M + 1)
+    k = gpsig_amd.SignatureRBF(L * D, D, M)
+    k.variances = torch.tensor(var, device=DEV, requires_grad=True)
+    Zt = torch.tensor(Z, device=DEV, requires_grad=True)
+    Xt = torch.tensor(X.reshape(N, -1), device=DEV, requires_grad=True)
+    Kzz, Kzx, Kxx = k.K_tens_n_seq_covs(Zt, Xt, full_X_cov=True)
+    ((Kzz * torch.as_tensor(G1, device=DEV)).sum() + (Kzx * torch.as_tensor(G2, device=DEV)).sum()
+     + (Kxx * torch.as_tensor(G3, device=DEV)).sum()).backward()
+    Zr, Xr, vr = (torch.tensor(Z, requires_grad=True), torch.tensor(X, requires_grad=True),
+                  torch.tensor(var, requires_grad=True))
+    Kzz_r = (ar.k_tens(Zr, M) * vr[:, None, None]).sum(0)
+    Kzx_r = ar.K_tens_vs_seq(Zr, Xr, M, scale=vr)
+    Kxx_r = ar.K(Xr, None, M, scale=vr)
+    ((Kzz_r * torch.tensor(G1)).sum() + (Kzx_r * torch.tensor(G2)).sum() + (Kxx_r * torch.tensor(G3)).sum()).backward()
+    assert norm_rel_err(Zt.grad.cpu().numpy(), Zr.grad.numpy()) < GTOL
+    assert norm_rel_err(Xt.grad.reshape(X.shape).cpu().numpy(), Xr.grad.numpy()) < GTOL
+    assert norm_rel_err(k.variances.grad.cpu().numpy(), vr.grad.numpy()) < GTOL

@@ -82,6 +82,40 @@ def test_K_tens_n_seq_covs_vs_oracle(full_X_cov):
         assert (norm_rel_err(a.cpu().numpy(), b, axis_levels=True) < TOL).all()
 
 
+@pytest.mark.parametrize("full_X_cov", [False, True])
+@pytest.mark.parametrize("normalization", [True, False])
+def test_K_tens_n_seq_covs_unnormalised_and_sum(full_X_cov, normalization):
+    import gpsig_amd
+    g = golden("tensors.npz")
+    X, M = g["X"], int(g["num_levels"])
+    N, L, D = X.shape
+    Z = g["Z"] * 0.3
+    var = np.linspace(0.5, 1.5, M + 1)
+    k = gpsig_amd.SignatureRBF(L * D, D, M, normalization=normalization, variances=var)
+    ref = kr.SignatureKernelRef(L * D, D, M, normalization=normalization, variances=var)
+    got = k.K_tens_n_seq_covs(t(Z), t(X.reshape(N, -1)), full_X_cov=full_X_cov)
+    exp = ref.K_tens_n_seq_covs(Z, X.reshape(N, -1), full_X_cov=full_X_cov)
+    for a, b in zip(got, exp):
+        assert norm_rel_err(a.cpu().numpy(), b) < TOL
+
+
+@pytest.mark.parametrize("full_X2_cov", [False, True])
+@pytest.mark.parametrize("normalization", [True, False])
+def test_K_seq_n_seq_covs_vs_oracle(full_X2_cov, normalization):
+    import gpsig_amd
+    g = golden("tensors.npz")
+    X, M = g["X"], int(g["num_levels"])
+    N, L, D = X.shape
+    X2 = np.cumsum(np.random.default_rng(5).standard_normal((7, L, D)), 1) / np.sqrt(L * D)
+    k = gpsig_amd.SignatureRBF(L * D, D, M, normalization=normalization)
+    ref = kr.SignatureKernelRef(L * D, D, M, normalization=normalization)
+    got = k.K_seq_n_seq_covs(t(X.reshape(N, -1)), t(X2.reshape(7, -1)), full_X2_cov=full_X2_cov, return_levels=True)
+    exp = ref.K_seq_n_seq_covs(X.reshape(N, -1), X2.reshape(7, -1), full_X2_cov=full_X2_cov, return_levels=True)
+    for a, b in zip(got, exp):
+        assert (norm_rel_err(a.cpu().numpy()[1:], b[1:], axis_levels=True) < TOL).all()
+        np.testing.assert_allclose(a.cpu().numpy()[0], b[0], rtol=1e-6)
+
+
 @pytest.mark.parametrize("emb", ["linear", "rbf"])
 def test_rescaled_vosf(emb):
     from gpsig_amd import ops
