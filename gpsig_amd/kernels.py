@@ -7,9 +7,11 @@ flattened ``(N, L*D)`` sequences.  The level recursion and its normalisation epi
 gfx950 kernels of gpsig_amd/libgpsig_amd.so; slicing, lags and lengthscale scaling (O(N*L*D)
 elementwise) run as torch ops on the same device.
 
-Not carried over ("Out of scope"): the low-rank Nystrom mode (``low_rank=True``
-raises NotImplementedError; signatures kept), GPflow Parameter transforms/priors (parameters are
-plain tensors here), and base kernels without a gfx950 seed (Cosine, Poly, Mix, Spectral, Matern*).
+The low-rank mode (``low_rank=True``: Nystrom features + randomized Hadamard projections,
+gpsig/low_rank_calculations.py) runs through gpsig_amd/low_rank_calculations.py (torch GEMMs /
+eigh on the device; the fused gfx950 Gram kernels are exact and are not used there).  Not carried
+over ("Out of scope"): GPflow Parameter transforms/priors (parameters are plain
+tensors here), and base kernels without a gfx950 seed (Cosine, Poly, Mix, Spectral, Matern*).
 """
 from __future__ import annotations
 
@@ -19,6 +21,7 @@ import torch
 from . import _lib as L
 from . import autograd as _ag
 from . import lags as _lags
+from . import low_rank_calculations as _lr
 from . import ops
 
 DEFAULT_JITTER = 1e-6  # GPflow 1.5.1 settings.jitter (third-party default, unpinned in this image)
@@ -56,9 +59,6 @@ class SignatureKernel:
         self.sigma = torch.tensor(1.0, dtype=torch.float64)
         self.low_rank, self.num_components, self.rank_bound, self.sparsity = self._validate_low_rank_params(
             low_rank, num_components, rank_bound, sparsity)
-        if self.low_rank:
-            raise NotImplementedError("low_rank=True (Nystrom + randomized projections, low_rank_calculations.py) "
-                                      "is out of scope of the gfx950 build; see DESIGN.md")
         if num_lags is None:
             self.num_lags = 0
         else:
@@ -177,12 +177,87 @@ class SignatureKernel:
         return ops.sig_diag(X, self.num_levels, self.order, self.base, self.difference, jitter=self.jitter,
                             rsqrt=True)
 
+    # ------------------------------------------------------------------ low-rank mode (kernels.py:240-312)
+    def _base_kern(self, X, X2=None):
+        """Base kernel matrix between point sets (kernels.py:946-957, 979-986, 1042-1044)."""
+        X2 = X if X2 is None else X2
+        if self.base == "rbf":
+            sq = (X ** 2).sum(-1)[:, None] + (X2 ** 2).sum(-1)[None, :] - 2.0 * X @ X2.T
+            return torch.exp(-sq / 2.0)
+        return X @ X2.T
+
+    def _lr_seeds(self, device):
+        return torch.randint(0, 2 ** 31 - 1, (max(self.num_levels - 1, 1), 2), device="cpu")
+
+    def _K_seq_lr_feat(self, X, nys_samples=None, seeds=None):
+        """kernels.py:240-262: (num_levels+1,) low-rank factors of scaled sequences X (N, L, D)."""
+        N, Ln, D = X.shape
+        X = X.to(torch.float64)
+        feat = _lr.Nystrom_map(X.reshape(N * Ln, D), self._base_kern, nys_samples, self.num_components)
+        feat = feat.reshape(N, Ln, -1)
+        if self.order != 1:
+            raise NotImplementedError('Low-rank mode not implemented for order higher than 1.')
+        return _lr.signature_kern_first_order_lr_feature(feat, self.num_levels, self.rank_bound, self.sparsity,
+                                                         seeds, difference=self.difference)
+
+    def _K_tens_lr_feat(self, Z, increments=False, nys_samples=None, seeds=None):
+        """kernels.py:286-312."""
+        if self.order > 1:
+            raise NotImplementedError('higher order not implemented yet for low-rank mode')
+        Z = Z.to(torch.float64)
+        LT, T, D = Z.shape[0], Z.shape[1], Z.shape[-1]
+        if increments:
+            f = _lr.Nystrom_map(Z.reshape(LT * T * 2, D), self._base_kern, nys_samples, self.num_components)
+            f = f.reshape(LT, T, 2, -1)
+            f = f[:, :, 1, :] - f[:, :, 0, :]
+        else:
+            f = _lr.Nystrom_map(Z.reshape(LT * T, D), self._base_kern, nys_samples, self.num_components)
+            f = f.reshape(LT, T, -1)
+        return _lr.tensor_kern_lr_feature(f, self.num_levels, self.rank_bound, self.sparsity, seeds)
+
+    def _nys_from(self, *sets):
+        """Shared Nystrom samples drawn from the union of point sets (kernels.py:443-446, 593-595)."""
+        pts = torch.cat([s.reshape(-1, s.shape[-1]).to(torch.float64) for s in sets], 0)
+        idx, _ = _lr._draw_indices(pts.shape[0], self.num_components, device=pts.device)
+        return pts[idx]
+
+    @staticmethod
+    def _gram_of(P, Q=None):
+        return torch.stack([p @ (p if Q is None else q).T for p, q in zip(P, P if Q is None else Q)], 0)
+
+    def _K_lowrank(self, Xs, X2s, return_levels):
+        """The low_rank branch of K (kernels.py:423-476), on the scaled sequences (the reference feeds
+        the unscaled X to _K_seq_lr_feat in K only, kernels.py:426,448 -- not reproduced)."""
+        if X2s is None:
+            Phi = self._K_seq_lr_feat(Xs)
+            K = self._gram_of(Phi)
+            if self.normalization:
+                K = K + self.jitter * torch.eye(K.shape[1], dtype=K.dtype, device=K.device)[None]
+                d = torch.sqrt(torch.diagonal(K, dim1=1, dim2=2))
+                K = K / (d[:, :, None] * d[:, None, :])
+        else:
+            seeds = self._lr_seeds(Xs.device)
+            nys = self._nys_from(Xs, X2s)
+            Phi = self._K_seq_lr_feat(Xs, nys, seeds)
+            Phi2 = self._K_seq_lr_feat(X2s, nys, seeds)
+            K = self._gram_of(Phi, Phi2)
+            if self.normalization:
+                d1 = torch.sqrt(torch.stack([(p ** 2).sum(-1) for p in Phi], 0) + self.jitter)
+                d2 = torch.sqrt(torch.stack([(p ** 2).sum(-1) for p in Phi2], 0) + self.jitter)
+                K = K / (d1[:, :, None] * d2[:, None, :])
+        K = K * (self.sigma * self.variances).to(K.device, K.dtype)[:, None, None]
+        return K if return_levels else K.sum(0)
+
     # ------------------------------------------------------------------ public API
     def K(self, X, X2=None, presliced=False, return_levels=False, presliced_X=False, presliced_X2=False):
         """kernels.py:402-477: (N, N2) or (num_levels+1, N, N2) with return_levels."""
         if presliced:
             presliced_X = presliced_X2 = True
         dt = self._out_dtype(X)
+        if self.low_rank:
+            Xs = self._prep(X, presliced_X)
+            X2s = None if X2 is None else self._prep(X2, presliced_X2)
+            return self._K_lowrank(Xs, X2s, return_levels).to(dt)
         Xs = self._prep(X, presliced_X)
         X2s = None if X2 is None else self._prep(X2, presliced_X2)
         scale = (self.sigma * self.variances).to(Xs.device)
@@ -208,6 +283,10 @@ class SignatureKernel:
                 return sv[:, None].repeat(1, N)
             return torch.full((N,), float(sv.sum()), dtype=dt, device=Xt.device)
         Xs = self._prep(Xt, presliced)
+        if self.low_rank:
+            Kd = torch.stack([(p ** 2).sum(-1) for p in self._K_seq_lr_feat(Xs)], 0)
+            Kd = Kd * (self.sigma * self.variances).to(Xs.device, Kd.dtype)[:, None]
+            return (Kd if return_levels else Kd.sum(0)).to(dt)
         Kd = self._K_seq_diag(Xs) * (self.sigma * self.variances).to(Xs.device, torch.float32)[:, None]
         return (Kd if return_levels else Kd.sum(0)).to(dt)
 
@@ -233,7 +312,11 @@ class SignatureKernel:
         Zt = _as_tensor(Z)
         dt = self._out_dtype(Z)
         Zs = self._apply_scaling_to_incremental_tensors(Zt) if increments else self._apply_scaling_to_tensors(Zt)
-        K = self._K_tens(Zs, increments) * (self.sigma * self.variances).to(Zs.device, torch.float32)[:, None, None]
+        if self.low_rank:
+            K = self._gram_of(self._K_tens_lr_feat(Zs, increments))
+        else:
+            K = self._K_tens(Zs, increments)
+        K = K * (self.sigma * self.variances).to(Zs.device, K.dtype)[:, None, None]
         return (K if return_levels else K.sum(0)).to(dt)
 
     def K_tens_vs_seq(self, Z, X, return_levels=False, increments=False, presliced=False):
@@ -242,11 +325,23 @@ class SignatureKernel:
         dt = self._out_dtype(X)
         Xs = self._prep(X, presliced)
         Zs = self._apply_scaling_to_incremental_tensors(Zt) if increments else self._apply_scaling_to_tensors(Zt)
-        Kzx = self._K_tens_vs_seq(Zs, Xs, increments)
-        if self.normalization:
-            Kzx = Kzx * self._rs_diff(Xs)[:, None, :]
-        Kzx = Kzx * (self.sigma * self.variances).to(Xs.device, torch.float32)[:, None, None]
+        if self.low_rank:
+            PhiZ, PhiX = self._lr_tens_seq_feats(Zs, Xs, increments)
+            Kzx = self._gram_of(PhiZ, PhiX)
+            if self.normalization:
+                Kzx = Kzx / torch.sqrt(torch.stack([(p ** 2).sum(-1) for p in PhiX], 0) + self.jitter)[:, None, :]
+        else:
+            Kzx = self._K_tens_vs_seq(Zs, Xs, increments)
+            if self.normalization:
+                Kzx = Kzx * self._rs_diff(Xs)[:, None, :]
+        Kzx = Kzx * (self.sigma * self.variances).to(Xs.device, Kzx.dtype)[:, None, None]
         return (Kzx if return_levels else Kzx.sum(0)).to(dt)
+
+    def _lr_tens_seq_feats(self, Zs, Xs, increments):
+        """Shared seeds and Nystrom samples for tensors and sequences (kernels.py:592-598, 645-652)."""
+        seeds = self._lr_seeds(Xs.device)
+        nys = self._nys_from(Zs, Xs)
+        return self._K_tens_lr_feat(Zs, increments, nys, seeds), self._K_seq_lr_feat(Xs, nys, seeds)
 
     def _sv(self, device):
         """sigma * variances as float32 on device, differentiable in variances."""
@@ -263,6 +358,8 @@ class SignatureKernel:
         Xs = self._prep(X, presliced)
         N = Xs.shape[0]
         Zs = self._apply_scaling_to_incremental_tensors(Zt) if increments else self._apply_scaling_to_tensors(Zt)
+        if self.low_rank:
+            return self._lr_tens_n_seq_covs(Zs, Xs, full_X_cov, return_levels, increments, dt)
         sv = self._sv(Xs.device)
         Kzz = self._K_tens(Zs, increments) * sv[:, None, None]
         Kzx = self._K_tens_vs_seq(Zs, Xs, increments)
@@ -288,6 +385,8 @@ class SignatureKernel:
         Xs = self._prep(X, True)  # reference slices only X2 here (kernels.py:712-713)
         X2s = self._prep(X2, presliced)
         N2 = X2s.shape[0]
+        if self.low_rank:
+            return self._lr_seq_n_seq_covs(Xs, X2s, full_X2_cov, return_levels, dt)
         sv = self._sv(Xs.device)
         Kxx = self._gram_levels(Xs)
         Kxx2 = self._gram_levels(Xs, X2s)
@@ -298,6 +397,68 @@ class SignatureKernel:
         else:
             Kd = self._K_seq_diag(X2s) * sv[:, None]
         out = (Kxx, Kxx2, Kd)
+        if not return_levels:
+            out = tuple(o.sum(0) for o in out)
+        return tuple(o.to(dt) for o in out)
+
+    def _lr_norm_sym(self, Phi):
+        """Gram of low-rank factors with jitter + diagonal normalisation (kernels.py:431-434), and the
+        square roots of its diagonal."""
+        K = self._gram_of(Phi)
+        if not self.normalization:
+            return K, None
+        K = K + self.jitter * torch.eye(K.shape[1], dtype=K.dtype, device=K.device)[None]
+        d = torch.sqrt(torch.diagonal(K, dim1=1, dim2=2))
+        return K / (d[:, :, None] * d[:, None, :]), d
+
+    def _lr_tens_n_seq_covs(self, Zs, Xs, full_X_cov, return_levels, increments, dt):
+        """Low-rank branch of K_tens_n_seq_covs (kernels.py:645-704)."""
+        N = Xs.shape[0]
+        PhiZ, PhiX = self._lr_tens_seq_feats(Zs, Xs, increments)
+        sv = (self.sigma * self.variances).to(Xs.device, torch.float64)
+        Kzz = self._gram_of(PhiZ) * sv[:, None, None]
+        Kzx = self._gram_of(PhiZ, PhiX)
+        if full_X_cov:
+            Kxx, d = self._lr_norm_sym(PhiX)
+            if d is not None:
+                Kzx = Kzx / d[:, None, :]
+            Kxx = Kxx * sv[:, None, None]
+        else:
+            Kd = torch.stack([(p ** 2).sum(-1) for p in PhiX], 0)
+            if self.normalization:
+                Kzx = Kzx / torch.sqrt(Kd + self.jitter)[:, None, :]
+                Kxx = sv[:, None].repeat(1, N)
+            else:
+                Kxx = Kd * sv[:, None]
+        out = (Kzz, Kzx * sv[:, None, None], Kxx)
+        if not return_levels:
+            out = tuple(o.sum(0) for o in out)
+        return tuple(o.to(dt) for o in out)
+
+    def _lr_seq_n_seq_covs(self, Xs, X2s, full_X2_cov, return_levels, dt):
+        """Low-rank branch of K_seq_n_seq_covs (kernels.py:720-794, intended semantics)."""
+        N2 = X2s.shape[0]
+        seeds = self._lr_seeds(Xs.device)
+        nys = self._nys_from(Xs, X2s)
+        Phi, Phi2 = self._K_seq_lr_feat(Xs, nys, seeds), self._K_seq_lr_feat(X2s, nys, seeds)
+        sv = (self.sigma * self.variances).to(Xs.device, torch.float64)
+        Kxx, d = self._lr_norm_sym(Phi)
+        Kxx2 = self._gram_of(Phi, Phi2)
+        if d is not None:
+            Kxx2 = Kxx2 / d[:, :, None]
+        if full_X2_cov:
+            Kd, d2 = self._lr_norm_sym(Phi2)
+            if d2 is not None:
+                Kxx2 = Kxx2 / d2[:, None, :]
+            Kd = Kd * sv[:, None, None]
+        else:
+            Kd = torch.stack([(p ** 2).sum(-1) for p in Phi2], 0)
+            if self.normalization:
+                Kxx2 = Kxx2 / torch.sqrt(Kd + self.jitter)[:, None, :]
+                Kd = sv[:, None].repeat(1, N2)
+            else:
+                Kd = Kd * sv[:, None]
+        out = (Kxx * sv[:, None, None], Kxx2 * sv[:, None, None], Kd)
         if not return_levels:
             out = tuple(o.sum(0) for o in out)
         return tuple(o.to(dt) for o in out)
