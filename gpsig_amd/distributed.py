@@ -9,7 +9,10 @@ has no distributed code; this is the north_star's multi-GPU path:
     the Gram work), so the only data-path collective is ONE all_gather_into_tensor of the finished,
     normalised row blocks, after which a gfx950 kernel mirrors the lower triangle
     (gpsig_sym_assemble);
-  * cross K(X, X2): the N1 rows are cut into P equal blocks, one all-gather.
+  * cross K(X, X2): the N1 rows are cut into P equal blocks, one all-gather;
+  * the PDE Gram (kernels_pde K) shards the same two ways; the inducing-tensor Kuf (K_tens_vs_seq)
+    shards its sequences (columns): each rank evaluates and normalises a contiguous block of
+    sequences (the normalisation is per sequence, no collective), one all-gather of the blocks.
 
 The compute and assembly steps are injectable so tests can run the partition / gather / assembly
 logic on CPU with the gloo backend (tests/test_distributed.py); the product path uses the HIP ops.
@@ -118,6 +121,73 @@ def sharded_cross_gram(X: torch.Tensor, X2: torch.Tensor, num_levels: int, *, ou
         dist.all_gather_into_tensor(g.view(world * levels * R, n2), local.reshape(levels * R, n2), group=group)
         full = g.permute(1, 0, 2, 3).reshape(levels, world * R, n2)[:, :n1]
     return full[0] if out_mode == L.OUT_NORM_SUM else full
+
+
+def _pde_compute(X, levels_out, rows, out, out_row0, num_levels=None, out_mode=None, dyadic=0, solver=1):
+    return ops.pde_gram(X, None, dyadic, solver, rows=rows, out=out[0], out_row0=out_row0)
+
+
+def sharded_pde_gram(X: torch.Tensor, X2: torch.Tensor | None = None, dyadic: int = 0, solver: int = 1, *,
+                     group=None, compute=None, assemble=None) -> torch.Tensor:
+    """PDE signature-kernel Gram (gpsig_pde_gram) row-sharded over the process group; (n1, n2) on
+    every rank.  compute(X, [X2,] levels, rows, out, out_row0, **kw) is injectable for CPU tests."""
+    if X2 is None:
+        return sharded_sym_gram(X, 0, out_mode=L.OUT_NORM_SUM, group=group, compute=compute or _pde_compute,
+                                assemble=assemble, dyadic=dyadic, solver=solver)
+
+    def cross(Xa, Xb, levels, rows, out, out_row0, num_levels=None, out_mode=None, **kw):
+        if rows[1] > rows[0]:
+            ops.pde_gram(Xa, Xb, dyadic, solver, rows=rows, out=out[0], out_row0=out_row0)
+
+    return sharded_cross_gram(X, X2, 0, out_mode=L.OUT_NORM_SUM, group=group, compute=compute or cross)
+
+
+def column_blocks(n: int, world: int):
+    """P contiguous blocks of ceil(n / P) sequences; block r = [r*C, min(n, (r+1)*C))."""
+    C = int(math.ceil(n / world))
+    return [(min(r * C, n), min((r + 1) * C, n)) for r in range(world)], C
+
+
+def sharded_columns(fn, X: torch.Tensor, group=None) -> torch.Tensor:
+    """Evaluate fn on this rank's contiguous block of sequences X[c0:c1] (fn returns (..., c1-c0)),
+    all-gather the blocks along the last axis; the full (..., n) result on every rank."""
+    rank, world = _world(group)
+    n = X.shape[0]
+    if world == 1:
+        return fn(X)
+    blocks, C = column_blocks(n, world)
+    c0, c1 = blocks[rank]
+    part = fn(X[c0:c1]) if c1 > c0 else None
+    lead = part.shape[:-1] if part is not None else None
+    # every rank needs the output's leading shape and dtype: take them from a 1-sequence evaluation
+    if part is None:
+        probe = fn(X[:1])
+        lead, dtype = probe.shape[:-1], probe.dtype
+    else:
+        dtype = part.dtype
+    local = torch.zeros((*lead, C), dtype=dtype, device=X.device)
+    if part is not None:
+        local[..., :c1 - c0] = part
+    g = torch.empty((world, *lead, C), dtype=dtype, device=X.device)
+    dist.all_gather_into_tensor(g.view(world * local.numel()), local.contiguous().view(-1), group=group)
+    full = g.movedim(0, -2).reshape(*lead, world * C)
+    return full[..., :n]
+
+
+def sharded_K_tens_vs_seq(kern, Z, X, return_levels=False, increments=False, group=None):
+    """SignatureKernel.K_tens_vs_seq (gpsig/kernels.py:571-620) with the sequences sharded over the
+    process group (normalisation is per sequence: no collective besides the all-gather)."""
+    Xt = X if isinstance(X, torch.Tensor) else torch.as_tensor(X, device="cuda")
+    return sharded_columns(lambda Xb: kern.K_tens_vs_seq(Z, Xb, return_levels=return_levels,
+                                                          increments=increments), Xt, group)
+
+
+def sharded_pde_K(kern, X, X2=None, group=None):
+    """UntruncSignatureKernel.K (PDE cross Gram) row-sharded over the process group."""
+    Xs = kern._prep(X)
+    X2s = None if X2 is None else kern._prep(X2)
+    K = sharded_pde_gram(Xs, X2s, kern.order, kern.solver, group=group)
+    return (float(kern.sigma) * K).to(kern._dt(X))
 
 
 def sharded_K(kern, X, X2=None, return_levels=False, group=None):

@@ -106,3 +106,75 @@ def test_row_offsets_layout():
     # every row maps to a distinct B*n-aligned slot inside (world, 2, levels, B, n)
     slots = sorted(int(o) // n for o in off)
     assert len(set(slots)) == n and max(off) < world * 2 * levels * B * n
+
+
+def _run_world2(target, *args):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=target, args=(r, 2, port, q) + args) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = dict(q.get(timeout=120) for _ in procs)
+    for p in procs:
+        p.join(timeout=60)
+    return res
+
+
+def _pde_worker(rank, world, port, q, n, cross):
+    from oracle import pde
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    rng = np.random.default_rng(1)
+    X = torch.as_tensor(np.cumsum(rng.standard_normal((n, 9, 2)), 1) * 0.3, dtype=torch.float32)
+    if cross:
+        X2 = X[:5] * 0.7
+
+        def comp(Xa, Xb, levels, rows, out, out_row0, **kw):
+            r0, r1 = rows
+            if r1 > r0:
+                out[0, r0 - out_row0:r1 - out_row0] = torch.as_tensor(
+                    pde.pde_gram(Xa[r0:r1].double().numpy(), Xb.double().numpy(), 1, 1), dtype=torch.float32)
+
+        res = D.sharded_pde_gram(X, X2, 1, 1, compute=comp)
+    else:
+        full = torch.as_tensor(pde.pde_gram(X.double().numpy(), None, 1, 1), dtype=torch.float32)[None]
+        res = D.sharded_pde_gram(X, None, 1, 1, compute=lambda *a, **k: _compute_sym(*a, full=full, **k),
+                                 assemble=_assemble_torch)
+    q.put((rank, res.numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("cross", [False, True])
+def test_sharded_pde_gram_world2(cross):
+    from oracle import pde
+    n = 11
+    res = _run_world2(_pde_worker, n, cross)
+    rng = np.random.default_rng(1)
+    X = np.cumsum(rng.standard_normal((n, 9, 2)), 1) * 0.3
+    X = X.astype(np.float32).astype(np.float64)
+    exp = pde.pde_gram(X, (X[:5] * 0.7).astype(np.float32).astype(np.float64) if cross else None, 1, 1)
+    for r in (0, 1):
+        np.testing.assert_allclose(res[r], exp, rtol=1e-5, atol=1e-6)
+
+
+def _cols_worker(rank, world, port, q, n):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    X = torch.arange(n * 3, dtype=torch.float32).reshape(n, 3)
+    fn = lambda Xb: torch.stack([Xb.sum(1), Xb[:, 0] * 2.0], 0)[None]  # (1, 2, nb) per block  # noqa: E731
+    q.put((rank, D.sharded_columns(fn, X).numpy()))
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("n", [1, 7, 10])
+def test_sharded_columns_world2(n):
+    res = _run_world2(_cols_worker, n)
+    X = torch.arange(n * 3, dtype=torch.float32).reshape(n, 3)
+    exp = torch.stack([X.sum(1), X[:, 0] * 2.0], 0)[None].numpy()
+    for r in (0, 1):
+        np.testing.assert_allclose(res[r], exp)
