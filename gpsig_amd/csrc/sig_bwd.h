@@ -350,9 +350,10 @@ __global__ __launch_bounds__(256) void sig_bwd_kernel(BwdArgs p) {
     }
     wave_sum_last_n<DP + 1>(s);
     if (lane == 63) {
-      for (int k = 0; k < d; ++k) {
+#pragma unroll
+      for (int k = 0; k < DP; ++k) {  // compile-time indices (a runtime bound would put s, xi in scratch)
         const float v = RBF ? __builtin_fmaf(-s[DP], xi[k], s[k]) : s[k];
-        unsafeAtomicAdd(gxa + (long long)pi * d + k, v);
+        if (k < d) unsafeAtomicAdd(gxa + (long long)pi * d + k, v);
       }
     }
   };
@@ -445,9 +446,10 @@ __global__ __launch_bounds__(256) void sig_bwd_kernel(BwdArgs p) {
     for (int w = 0; w < W; ++w) {
       const int j = gl * W + w;
       if (!ptv[w]) continue;
-      for (int k = 0; k < d; ++k) {
+#pragma unroll
+      for (int k = 0; k < DP; ++k) {
         const float v = RBF ? __builtin_fmaf(-A[w], y[w][k], B[w][k]) : B[w][k];
-        unsafeAtomicAdd(gyb + (long long)j * d + k, v);
+        if (k < d) unsafeAtomicAdd(gyb + (long long)j * d + k, v);
       }
     }
   }
