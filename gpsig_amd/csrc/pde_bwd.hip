@@ -30,7 +30,7 @@ struct PdeBwdArgs {
   double *grid;       // scratch: (row_end - row_begin) * [n2 | 1] grids of (I+1) x (J+1)
 };
 
-template <int DP, int W, bool REV>
+template <int DP, int W, bool REV, bool COLS>
 __global__ __launch_bounds__(256) void pde_bwd_kernel(PdeBwdArgs p) {
   extern __shared__ __attribute__((aligned(16))) double ldsd[];
   const int lane = threadIdx.x & 63;
@@ -113,8 +113,16 @@ __global__ __launch_bounds__(256) void pde_bwd_kernel(PdeBwdArgs p) {
       double grow[DP];
 #pragma unroll
       for (int k = 0; k < DP; ++k) grow[k] = 0.0;
-      const double *krr = REV ? nullptr : p.grid + pidx * (long long)(I + 1) * (J + 1) +
-                                               (long long)(I - 1 - i) * (J + 1) + (J - 1);
+      // K_rev[I-1-i][J-1-c] of the lane's columns, loaded before the column loop
+      double kr[W];
+      if constexpr (!REV) {
+        const double *krr = p.grid + pidx * (long long)(I + 1) * (J + 1) + (long long)(I - 1 - i) * (J + 1) + (J - 1);
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          const int c = lane * W + w;
+          kr[w] = c < J ? krr[-c] : 0.0;
+        }
+      }
 #pragma unroll
       for (int w = 0; w < W; ++w) {
         const int c = lane * W + w;
@@ -135,11 +143,11 @@ __global__ __launch_bounds__(256) void pde_bwd_kernel(PdeBwdArgs p) {
             grid[(long long)(i + 1) * (J + 1) + c + 1] = kn;
           } else {
             // KK[i][c] = K[i][c] * K_rev[I-1-i][J-1-c]
-            const double kk = cor * krr[-c];
+            const double kk = cor * kr[w];
 #pragma unroll
             for (int k = 0; k < DP; ++k) {
               grow[k] = __builtin_fma(kk, (double)dy[w][k], grow[k]);
-              gcol[w][k] = __builtin_fma(kk, (double)dxv[k], gcol[w][k]);
+              if constexpr (COLS) gcol[w][k] = __builtin_fma(kk, (double)dxv[k], gcol[w][k]);
             }
           }
           cor = upw;
@@ -169,7 +177,7 @@ __global__ __launch_bounds__(256) void pde_bwd_kernel(PdeBwdArgs p) {
       const double gc = r < IC ? gacc[r * DP + k] : 0.0;
       unsafeAtomicAdd(gxa + (long long)r * d + k, (float)(sx * (gp - gc)));
     }
-  if (diag) return;
+  if (diag || !COLS) return;
   // columns: H[j] = 4^-n sum over the fine columns of coarse column j; dK/dy_j = H[j-1] - H[j]
   const double sy = inv_factor * (double)g;
   float *gyb = p.gY + (long long)b * p.l2 * d;
@@ -193,8 +201,12 @@ static int launch_pde_bwd(const PdeBwdArgs &a, long long nblocks, hipStream_t s)
   } else {
     const size_t lds = (size_t)4 * (a.l1 - 1) * DP * 2 * sizeof(double);
     if (lds > 160 * 1024) return GPSIG_EUNSUPPORTED;
-    hipLaunchKernelGGL((pde_bwd_kernel<DP, W, true>), dim3((unsigned)nblocks), dim3(256), lds, s, a);
-    hipLaunchKernelGGL((pde_bwd_kernel<DP, W, false>), dim3((unsigned)nblocks), dim3(256), lds, s, a);
+    hipLaunchKernelGGL((pde_bwd_kernel<DP, W, true, false>), dim3((unsigned)nblocks), dim3(256), lds, s, a);
+    // the column (dK/dy) accumulators only for cross pairs; k(x, x) takes twice the row part
+    if (a.pair_mode == GPSIG_PAIRS_DIAG)
+      hipLaunchKernelGGL((pde_bwd_kernel<DP, W, false, false>), dim3((unsigned)nblocks), dim3(256), lds, s, a);
+    else
+      hipLaunchKernelGGL((pde_bwd_kernel<DP, W, false, true>), dim3((unsigned)nblocks), dim3(256), lds, s, a);
     return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
   }
 }

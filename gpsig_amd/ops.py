@@ -197,7 +197,7 @@ def pde_gram(X: torch.Tensor, Y: torch.Tensor | None = None, dyadic: int = 0, so
     return out
 
 
-PDE_VJP_SCRATCH = 1 << 30  # bytes of fp64 K_rev grids per launch (rows are chunked to fit)
+PDE_VJP_SCRATCH = 4 << 30  # bytes of fp64 K_rev grids per launch (rows are chunked to fit)
 
 
 def pde_diag_vjp(X: torch.Tensor, gout: torch.Tensor, dyadic: int = 0, solver: int = 1,
