@@ -24,11 +24,11 @@ struct SigFeatArgs {
 
 __global__ __launch_bounds__(256) void sig_features_kernel(SigFeatArgs a) {
   extern __shared__ __attribute__((aligned(16))) float S[];  // [h (d) | level 1 | level 2 | ...]
-  const int path = blockIdx.x, tid = threadIdx.x;
+  const int path = blockIdx.x, tid = threadIdx.x, nth = blockDim.x;
   const int d = a.d, M = a.depth;
   float *h = S;
   float *lev = S + d;
-  for (int e = tid; e < a.total; e += 256) lev[e] = 0.0f;
+  for (int e = tid; e < a.total; e += nth) lev[e] = 0.0f;
   int off[17], sz[17];  // level m at lev + off[m], d^m entries
   off[1] = 0;
   sz[0] = 1;
@@ -43,7 +43,7 @@ __global__ __launch_bounds__(256) void sig_features_kernel(SigFeatArgs a) {
     __syncthreads();
     for (int m = M; m >= 1; --m) {
       float *Sm = lev + off[m];
-      for (int e = tid; e < sz[m]; e += 256) {
+      for (int e = tid; e < sz[m]; e += nth) {
         float acc = 0.0f, P = 1.0f, fact = 1.0f;
         int pre = e;
         for (int j = m - 1; j >= 0; --j) {
@@ -60,7 +60,7 @@ __global__ __launch_bounds__(256) void sig_features_kernel(SigFeatArgs a) {
     }
   }
   float *o = a.out + (long long)path * a.total;
-  for (int e = tid; e < a.total; e += 256) o[e] = lev[e];
+  for (int e = tid; e < a.total; e += nth) o[e] = lev[e];
 }
 
 // ------------------------------------------------------------------------------------ backward
@@ -75,7 +75,7 @@ __global__ __launch_bounds__(256) void sig_features_kernel(SigFeatArgs a) {
 __global__ __launch_bounds__(256) void sig_features_bwd_kernel(SigFeatArgs a, const float *__restrict__ gout,
                                                                float *__restrict__ gX) {
   extern __shared__ __attribute__((aligned(16))) float sh[];
-  const int path = blockIdx.x, tid = threadIdx.x;
+  const int path = blockIdx.x, tid = threadIdx.x, nth = blockDim.x;
   const int d = a.d, M = a.depth, tot = a.total;
   float *h = sh, *gh = sh + d;
   float *lev = sh + 2 * d, *adj = lev + tot, *gE = adj + tot;
@@ -89,7 +89,7 @@ __global__ __launch_bounds__(256) void sig_features_bwd_kernel(SigFeatArgs a, co
   const float *x = a.X + (long long)path * a.l * d;
   float *gx = gX + (long long)path * a.l * d;
   const float *g = gout + (long long)path * tot;
-  for (int e = tid; e < tot; e += 256) {
+  for (int e = tid; e < tot; e += nth) {
     lev[e] = 0.0f;
     adj[e] = g[e];
   }
@@ -97,7 +97,7 @@ __global__ __launch_bounds__(256) void sig_features_bwd_kernel(SigFeatArgs a, co
   auto chen = [&]() {
     for (int m = M; m >= 1; --m) {
       float *Sm = lev + off[m];
-      for (int e = tid; e < sz[m]; e += 256) {
+      for (int e = tid; e < sz[m]; e += nth) {
         float acc = 0.0f, P = 1.0f, fact = 1.0f;
         int pre = e;
         for (int j = m - 1; j >= 0; --j) {
@@ -140,7 +140,7 @@ __global__ __launch_bounds__(256) void sig_features_bwd_kernel(SigFeatArgs a, co
     __syncthreads();
     // dE_r[v] for r = 1..M
     for (int r = 1; r <= M; ++r)
-      for (int v = tid; v < sz[r]; v += 256) {
+      for (int v = tid; v < sz[r]; v += nth) {
         float acc = 0.0f;
         for (int m = r; m <= M; ++m) {
           const int nu = sz[m - r];
@@ -155,7 +155,7 @@ __global__ __launch_bounds__(256) void sig_features_bwd_kernel(SigFeatArgs a, co
     __syncthreads();
     // dh from dE (LDS float atomics into d slots)
     for (int r = 1; r <= M; ++r)
-      for (int v = tid; v < sz[r]; v += 256) {
+      for (int v = tid; v < sz[r]; v += nth) {
         const float ge = gE[off[r] + v];
         float fact = 1.0f;
         for (int p = 1; p <= r; ++p) fact *= (float)p;
@@ -175,7 +175,7 @@ __global__ __launch_bounds__(256) void sig_features_bwd_kernel(SigFeatArgs a, co
       }
     // dS_j[u] = sum_{m>=j} sum_v dT_m[u v] E_{m-j}[v], ascending j in place
     for (int j = 1; j <= M; ++j) {
-      for (int u = tid; u < sz[j]; u += 256) {
+      for (int u = tid; u < sz[j]; u += nth) {
         float acc = adj[off[j] + u];
         for (int m = j + 1; m <= M; ++m) {
           const int nv = sz[m - j];
@@ -210,7 +210,9 @@ extern "C" int gpsig_signature_vjp(const float *X, int n, int l, int d, int dept
   const size_t lds = (size_t)(3 * total + 2 * d) * sizeof(float);
   if (lds > 64 * 1024) return GPSIG_EUNSUPPORTED;
   SigFeatArgs a{X, n, l, d, depth, nullptr, (int)total};
-  hipLaunchKernelGGL(sig_features_bwd_kernel, dim3((unsigned)n), dim3(256), lds, s, a, gout, gX);
+  // one wave per path while the top level fits a few entries per lane (barriers stay wave-local)
+  const int nth = (total - (total - 1) / d) <= 256 ? 64 : 256;
+  hipLaunchKernelGGL(sig_features_bwd_kernel, dim3((unsigned)n), dim3(nth), lds, s, a, gout, gX);
   return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
 }
 
@@ -232,6 +234,7 @@ extern "C" int gpsig_signature(const float *X, int n, int l, int d, int depth, f
   const size_t lds = (size_t)(total + d) * sizeof(float);
   if (lds > 64 * 1024) return GPSIG_EUNSUPPORTED;
   SigFeatArgs a{X, n, l, d, depth, out, (int)total};
-  hipLaunchKernelGGL(sig_features_kernel, dim3((unsigned)n), dim3(256), lds, s, a);
+  const int nth = (total - (total - 1) / d) <= 256 ? 64 : 256;  // top level d^depth entries
+  hipLaunchKernelGGL(sig_features_kernel, dim3((unsigned)n), dim3(nth), lds, s, a);
   return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
 }
