@@ -90,10 +90,11 @@ struct TvsCell {
 // time difference k(z_k, x_{pt+1}) - k(z_k, x_pt) (difference=True, signature_algs.py:114); with
 // increments the component is the pair (z0, z1) and M = k(z1, x) - k(z0, x) (kernels.py:328-331).
 // kc carries k(z_k, x_pt) across cells for the RBF DIFF seed.
+// zs: this tensor's components staged in LDS, component k at zs + k * (incr ? 2d : d).
 template <int DP>
-GPSIG_DEV float tvs_seed(const TvsArgs &a, int k, int tt, const TvsCell<DP> &cl, float &kc) {
+GPSIG_DEV float tvs_seed(const TvsArgs &a, const float *zs, int k, const TvsCell<DP> &cl, float &kc) {
   const int d = a.d;
-  const float *zt = a.incr ? a.Z + (((long long)k * a.t + tt) * 2) * d : a.Z + ((long long)k * a.t + tt) * d;
+  const float *zt = zs + k * (a.incr ? 2 * d : d);
   if (!a.rbf) {
     float v = 0.f;
 #pragma unroll
@@ -163,6 +164,17 @@ __global__ __launch_bounds__(64) void tvs_kernel(TvsArgs a) {
   const int n = a.n, d = a.d, FC = 2 * d + 3, M = a.M, LT = a.lt;
   float *Ssum = lds + lane;            // Ssum[k * 64]: exclusive-in-time running sums per (level, stage)
   float *kc = lds + 64 * LT + lane;    // kc[k * 64]: RBF DIFF carried k(z_k, x_pt)
+  // the wave's tensor (uniform): staged in LDS -- broadcast reads instead of the serialised
+  // L2-latency vector loads the compiler emits for uniform global data it cannot prove invariant
+  float *zl = lds + 2 * 64 * LT;
+  {
+    const int zstride = a.incr ? 2 * d : d;
+    for (int e = lane; e < LT * zstride; e += 64) {
+      const int k = e / zstride, r = e % zstride;
+      zl[e] = a.Z[((long long)k * a.t + tt) * zstride + r];
+    }
+    __syncthreads();
+  }
   float K[TV_MMAX + 1];
 #pragma unroll
   for (int k = 0; k <= TV_MMAX; ++k) K[k] = 0.f;
@@ -195,13 +207,13 @@ __global__ __launch_bounds__(64) void tvs_kernel(TvsArgs a) {
     for (int i = 1; i <= M; ++i) {
       const int k0 = i * (i - 1) / 2;
       float kk = kc[k0 * 64];
-      const float m0 = tvs_seed<DP>(a, k0, tt, cl, kk);
+      const float m0 = tvs_seed<DP>(a, zl, k0, cl, kk);
       kc[k0 * 64] = kk;
       if (a.order <= 1) {
         float prev = m0;  // R_0(pt)
         for (int st = 1; st < i; ++st) {
           float kq = kc[(k0 + st) * 64];
-          const float mk = tvs_seed<DP>(a, k0 + st, tt, cl, kq);
+          const float mk = tvs_seed<DP>(a, zl, k0 + st, cl, kq);
           kc[(k0 + st) * 64] = kq;
           const float ss = Ssum[(k0 + st - 1) * 64];
           Ssum[(k0 + st - 1) * 64] = ss + prev;
@@ -220,7 +232,7 @@ __global__ __launch_bounds__(64) void tvs_kernel(TvsArgs a) {
 #pragma unroll
           for (int b = 0; b < TV_MMAX; ++b) tot += blk[b];
           float kq = kc[(k0 + st) * 64];
-          const float mk = tvs_seed<DP>(a, k0 + st, tt, cl, kq);
+          const float mk = tvs_seed<DP>(a, zl, k0 + st, cl, kq);
           kc[(k0 + st) * 64] = kq;
 #pragma unroll
           for (int b = TV_MMAX - 1; b >= 1; --b) blk[b] = (b < dn) ? mk * blk[b - 1] / (float)(b + 1) : 0.f;
@@ -319,12 +331,16 @@ __global__ __launch_bounds__(64) void rescaled_kernel(RsArgs a) {
   const int d = a.d, L = a.l;
   const float *x = a.X + (long long)nn * L * d;
   constexpr int LT = M * (M + 1) / 2;
-  // lambda of component r for this tensor (wave-uniform, read through the scalar cache); the ones
-  // tensor of the concatenation (kernels.py:812) is tt == T
-  auto lam = [&](int r, int q) -> float {
-    return (q < d) ? ((tt < a.t) ? a.Z[((long long)r * a.t + tt) * d + q] : 1.0f) : 0.f;
-  };
-  (void)LT;
+  // lambda of component r for this tensor (wave-uniform), staged in LDS once (the compiler would
+  // otherwise emit serialised vector loads for it inside the row loop); the ones tensor of the
+  // concatenation (kernels.py:812) is tt == T
+  __shared__ float lz[LT * DP];
+  for (int e = lane; e < LT * DP; e += 64) {
+    const int r = e / DP, q = e % DP;
+    lz[e] = (q < d) ? ((tt < a.t) ? a.Z[((long long)r * a.t + tt) * d + q] : 1.0f) : 0.f;
+  }
+  __syncthreads();
+  auto lam = [&](int r, int q) -> float { return lz[r * DP + q]; };
   // this lane's columns q0 = lane*W + w
   float xc[W][DP], dxc[W][DP];
   bool valid[W];
@@ -558,7 +574,7 @@ extern "C" int gpsig_tens_vs_seq(const float *Z, int lt, int t, int increments, 
   }
   TvsArgs a{Z, Ft, lt, t, n, l, d, num_levels, order, increments, difference, base_kind == GPSIG_BASE_RBF, out};
   dim3 grid((n + 63) / 64, t);
-  const size_t lds = (size_t)2 * 64 * lt * sizeof(float);
+  const size_t lds = ((size_t)2 * 64 * lt + (size_t)lt * (increments ? 2 : 1) * d) * sizeof(float);
   switch (DP) {
     case 4: hipLaunchKernelGGL(tvs_kernel<4>, grid, dim3(64), lds, s, a); break;
     case 8: hipLaunchKernelGGL(tvs_kernel<8>, grid, dim3(64), lds, s, a); break;
