@@ -531,7 +531,7 @@ static int dpad4(int d) { return d <= 4 ? 4 : d <= 8 ? 8 : d <= 16 ? 16 : d <= 3
 
 namespace gpsig {
 int tvs_pk_launch(const float *Z, int lt, int t, int increments, int d, const float *Ft, int n, int l, int M,
-                  float *out, float *Zp, hipStream_t s);
+                  float *out, float *Zp, bool rbf, hipStream_t s);
 size_t tvs_pk_zp_bytes(int lt, int t, int d);
 }  // namespace gpsig
 
@@ -567,9 +567,11 @@ extern "C" int gpsig_tens_vs_seq(const float *Z, int lt, int t, int increments, 
   float *Ft = static_cast<float *>(workspace);
   const long long tot = (long long)n * l;
   hipLaunchKernelGGL(tvs_features_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, X, n, l, d, Ft);
-  if (base_kind == GPSIG_BASE_RBF && difference && order == 1) {
+  if (difference && order == 1) {
+    // packed fast paths: RBF (exp-free recurrences) and linear
     float *Zp = reinterpret_cast<float *>(static_cast<char *>(workspace) + tvs_ft_bytes(n, l, d));
-    const int rc = tvs_pk_launch(Z, lt, t, increments, d, Ft, n, l, num_levels, out, Zp, s);
+    const int rc = tvs_pk_launch(Z, lt, t, increments, d, Ft, n, l, num_levels, out, Zp,
+                                 base_kind == GPSIG_BASE_RBF, s);
     if (rc != -1) return rc;
   }
   TvsArgs a{Z, Ft, lt, t, n, l, d, num_levels, order, increments, difference, base_kind == GPSIG_BASE_RBF, out};

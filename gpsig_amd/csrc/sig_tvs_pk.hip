@@ -229,39 +229,103 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(INCR ? GPSIG
   }
 }
 
+// Linear base kernel (kernels.py:979-986), difference=True: the seed of component k at time cell s is
+// <w_k, dx_s> with w_k = z_k (or z1_k - z0_k with increments), no state besides the running sums.
+template <int DP, int M, bool INCR>
+__global__ __launch_bounds__(64) void tvs_lin_kernel(TvsPkArgs a) {
+  constexpr int LT = M * (M + 1) / 2;
+  constexpr int ZS = tvs_zs<DP, INCR>();
+  constexpr int d = DP;
+  const int lane = threadIdx.x;
+  const int tt = blockIdx.y;
+  const int n = a.n, FC = 2 * d + 3;
+  const int s0 = blockIdx.x * 128 + lane, s1 = s0 + 64;
+  const int c0 = s0 < n ? s0 : n - 1, c1 = s1 < n ? s1 : n - 1;
+  __shared__ __attribute__((aligned(16))) float zl[LT * ZS];
+  for (int e = lane; e < LT * ZS; e += 64) zl[e] = a.Zp[(long long)tt * LT * ZS + e];
+  __syncthreads();
+  f2 Ss[LT], K[M + 1];
+#pragma unroll
+  for (int k = 0; k < LT; ++k) Ss[k] = splat2(0.f);
+#pragma unroll
+  for (int i = 0; i <= M; ++i) K[i] = splat2(0.f);
+  for (int s = 0; s + 1 < a.l; ++s) {
+    asm volatile("" ::: "memory");
+    f2 dx[DP];
+#pragma unroll
+    for (int q = 0; q < DP; ++q) {
+      const float *f = a.Ft + ((long long)s * FC + d + q) * n;
+      dx[q] = (f2){f[c0], f[c1]};
+    }
+#pragma unroll
+    for (int i = 1; i <= M; ++i) {
+      const int k0 = i * (i - 1) / 2;
+      f2 prev = splat2(0.f);
+#pragma unroll
+      for (int st = 0; st < i; ++st) {
+        const int k = k0 + st;
+        const float *w = zl + k * ZS + (INCR ? DP : 0);
+        f2 m = splat2(0.f);
+#pragma unroll
+        for (int q = 0; q < DP; ++q) m = fma2(dx[q], splat2(w[q]), m);
+        if (st == 0) {
+          prev = m;
+        } else {
+          const f2 ss = Ss[k - 1];
+          Ss[k - 1] = ss + prev;
+          prev = m * ss;
+        }
+      }
+      K[i] += prev;
+    }
+  }
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int sq = h ? s1 : s0;
+    if (sq < n) {
+      a.out[(long long)tt * n + sq] = 1.0f;
+#pragma unroll
+      for (int i = 1; i <= M; ++i) a.out[((long long)i * a.t + tt) * n + sq] = K[i][h];
+    }
+  }
+}
+
 template <int DP, int M, bool INCR>
 static int launch_tvs_pk(const float *Z, int lt, int t, int d, const float *Ft, int n, int l, float *out, float *Zp,
-                         hipStream_t s) {
+                         bool rbf, hipStream_t s) {
   hipLaunchKernelGGL((tvs_prep_kernel<DP, INCR>), dim3((unsigned)((lt * t + 255) / 256)), dim3(256), 0, s, Z, lt, t, d,
                      Zp);
   TvsPkArgs a{Zp, Ft, t, n, l, d, out};
-  hipLaunchKernelGGL((tvs_pk_kernel<DP, M, INCR>), dim3((unsigned)((n + 127) / 128), (unsigned)t), dim3(64), 0, s, a);
+  if (rbf)
+    hipLaunchKernelGGL((tvs_pk_kernel<DP, M, INCR>), dim3((unsigned)((n + 127) / 128), (unsigned)t), dim3(64), 0, s, a);
+  else
+    hipLaunchKernelGGL((tvs_lin_kernel<DP, M, INCR>), dim3((unsigned)((n + 127) / 128), (unsigned)t), dim3(64), 0, s, a);
   return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
 }
 
 template <int DP, bool INCR>
 static int tvs_pk_m(int M, const float *Z, int lt, int t, int d, const float *Ft, int n, int l, float *out, float *Zp,
-                    hipStream_t s) {
+                    bool rbf, hipStream_t s) {
   switch (M) {
-    case 1: return launch_tvs_pk<DP, 1, INCR>(Z, lt, t, d, Ft, n, l, out, Zp, s);
-    case 2: return launch_tvs_pk<DP, 2, INCR>(Z, lt, t, d, Ft, n, l, out, Zp, s);
-    case 3: return launch_tvs_pk<DP, 3, INCR>(Z, lt, t, d, Ft, n, l, out, Zp, s);
-    case 4: return launch_tvs_pk<DP, 4, INCR>(Z, lt, t, d, Ft, n, l, out, Zp, s);
-    case 5: return launch_tvs_pk<DP, 5, INCR>(Z, lt, t, d, Ft, n, l, out, Zp, s);
-    case 6: return launch_tvs_pk<DP, 6, INCR>(Z, lt, t, d, Ft, n, l, out, Zp, s);
+    case 1: return launch_tvs_pk<DP, 1, INCR>(Z, lt, t, d, Ft, n, l, out, Zp, rbf, s);
+    case 2: return launch_tvs_pk<DP, 2, INCR>(Z, lt, t, d, Ft, n, l, out, Zp, rbf, s);
+    case 3: return launch_tvs_pk<DP, 3, INCR>(Z, lt, t, d, Ft, n, l, out, Zp, rbf, s);
+    case 4: return launch_tvs_pk<DP, 4, INCR>(Z, lt, t, d, Ft, n, l, out, Zp, rbf, s);
+    case 5: return launch_tvs_pk<DP, 5, INCR>(Z, lt, t, d, Ft, n, l, out, Zp, rbf, s);
+    case 6: return launch_tvs_pk<DP, 6, INCR>(Z, lt, t, d, Ft, n, l, out, Zp, rbf, s);
     default: return -1;
   }
 }
 
 // -1: not covered by the fast path (the caller runs the general kernel)
 int tvs_pk_launch(const float *Z, int lt, int t, int increments, int d, const float *Ft, int n, int l, int M,
-                  float *out, float *Zp, hipStream_t s) {
+                  float *out, float *Zp, bool rbf, hipStream_t s) {
   if (M > 6 || d > 8 || l < 2) return -1;
   const int DP = d;
 #define GPSIG_TVS(dp)                                                               \
   case dp:                                                                          \
-    return increments ? tvs_pk_m<dp, true>(M, Z, lt, t, d, Ft, n, l, out, Zp, s)    \
-                      : tvs_pk_m<dp, false>(M, Z, lt, t, d, Ft, n, l, out, Zp, s);
+    return increments ? tvs_pk_m<dp, true>(M, Z, lt, t, d, Ft, n, l, out, Zp, rbf, s)    \
+                      : tvs_pk_m<dp, false>(M, Z, lt, t, d, Ft, n, l, out, Zp, rbf, s);
   switch (DP) {
     GPSIG_TVS(1) GPSIG_TVS(2) GPSIG_TVS(3) GPSIG_TVS(4) GPSIG_TVS(5) GPSIG_TVS(6) GPSIG_TVS(7) GPSIG_TVS(8)
     default: return -1;
