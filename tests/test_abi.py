@@ -61,3 +61,20 @@ def test_product_path_refuses_cpu_tensors():
     X = torch.zeros(2, 5, 3)
     with pytest.raises(gpsig_amd.GpsigError):
         ops.sig_diag(X, 3)
+
+
+def test_vjp_and_feature_entry_points_validate_arguments():
+    """The gradient / signature entry points reject null pointers and bad shapes before any HIP call."""
+    import gpsig_amd._lib as L
+    lib = L.load()
+    assert lib.gpsig_sig_gram_vjp(None, 4, 10, None, 4, 10, 3, 4, 0, 0, 0, 4, None, 0, None, None, None, 0.0,
+                                  None, None, None, None, None, None, 0, None) == L.GPSIG_EINVAL
+    assert lib.gpsig_tens_vs_seq_vjp(None, 6, 2, 0, 3, None, 4, 10, 3, 0, None, None, None, None, 0,
+                                     None) == L.GPSIG_EINVAL
+    assert lib.gpsig_tens_gram_vjp(None, 6, 2, 0, 3, 3, 0, None, None, None) == L.GPSIG_EINVAL
+    assert lib.gpsig_pde_vjp(None, 4, 10, None, 4, 10, 3, 0, 1, 0, 0, 4, None, None, None, None, 0,
+                             None) == L.GPSIG_EINVAL
+    assert lib.gpsig_signature(None, 4, 10, 3, 3, None, None) == L.GPSIG_EINVAL
+    assert lib.gpsig_signature_vjp(None, 4, 10, 3, 3, None, None, None) == L.GPSIG_EINVAL
+    assert lib.gpsig_signature_channels(5, 3) == 5 + 25 + 125
+    assert lib.gpsig_pde_vjp_workspace_bytes(2, 10, 10, 1) == 2 * 19 * 19 * 8

@@ -169,3 +169,14 @@ def test_full_size_properties_headline():
     exp = ref.K(X[idx].reshape(len(idx), -1), X[:40].reshape(40, -1))
     got = k.K(Xt[idx], Xt[:40]).cpu().numpy()
     assert norm_rel_err(got, exp) < TOL
+
+
+@pytest.mark.parametrize("case", ["channels", "levels", "length"])
+def test_unsupported_configurations_raise(case):
+    """Configurations outside the compiled instantiations fail loudly (GpsigError), never silently."""
+    import gpsig_amd
+    from gpsig_amd import ops
+    D, M, L = {"channels": (40, 3, 10), "levels": (3, 9, 10), "length": (4, 3, 600)}[case]
+    X = torch.zeros((2, L, D), device=DEV)
+    with pytest.raises(gpsig_amd.GpsigError):
+        ops.sig_gram(X, None, M)
