@@ -99,8 +99,11 @@ GPSIG_DEV void wave_sum_last_n(float (&v)[N]) {
   group_incl_scan_n<64, N>(v);
 }
 
+#ifndef GPSIG_BWD_WPE
+#define GPSIG_BWD_WPE 1
+#endif
 template <int DP, int W, int LP, int M, int SEED>
-__global__ __launch_bounds__(256) void sig_bwd_kernel(BwdArgs p) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_WPE))) void sig_bwd_kernel(BwdArgs p) {
   constexpr int FS = feat_stride(DP);
   constexpr int G = 64 / LP;
   constexpr bool RBF = (SEED == SEED_RBF_DIFF);
