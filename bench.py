@@ -79,6 +79,25 @@ def cpu_baseline(l, d, m, seconds=15.0, n_blk=8):
 
 
 # ----------------------------------------------------------------------------- main
+def hbm_copy_probe(dev, nbytes=1 << 30, reps=20):
+    """Achievable HBM bandwidth (GB/s): read + write bytes of a 1 GiB device-to-device copy, timed with
+    events after the measured steps (outside the timed region)."""
+    import torch
+    a = torch.empty(nbytes // 4, dtype=torch.float32, device=dev).fill_(1.0)
+    b = torch.empty_like(a)
+    for _ in range(3):
+        b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        b.copy_(a)
+    e1.record()
+    e1.synchronize()
+    gbs = 2.0 * nbytes * reps / (e0.elapsed_time(e1) / 1e3) / 1e9
+    del a, b
+    return gbs
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -89,6 +108,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-check", action="store_true")
+    ap.add_argument("--no-probe", action="store_true", help="skip the HBM copy-bandwidth probe")
     ap.add_argument("--backend", default="nccl",
                     help="process-group backend (nccl = RCCL; gloo only to rehearse N>1 ranks on one GPU)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r1_gram_counters.json"),
@@ -176,6 +196,7 @@ def main():
             prof = json.load(f)
         traffic = prof.get("hbm_bytes_per_launch")
 
+    probe = hbm_copy_probe(dev) if rank == 0 and not args.no_probe else None
     value = args.steps * n * n / elapsed
     out = {
         "metric": "sig-kernel Gram entries/sec (N, len L, dim D, level M); max-abs err vs ref",
@@ -198,7 +219,9 @@ def main():
                      "entries_per_launch": entries_per_launch,
                      # the fused kernel never materialises the tile: physically it is VALU-issue bound
                      "physical_bound": "valu", "valu_issue_util": prof.get("valu_issue_util"),
-                     "profile": os.path.relpath(args.traffic_json, ROOT) if prof else None},
+                     "profile": os.path.relpath(args.traffic_json, ROOT) if prof else None,
+                     # the datasheet peak and a measured device-to-device copy, both
+                     "peak_probe": probe, "frac_probe": achieved / probe if probe else None},
     }
     if rank == 0 and not args.no_check:
         # parity on a bounded subsample: the normalised Gram restricted to a subset S of the sequences

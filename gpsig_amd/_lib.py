@@ -47,7 +47,10 @@ SIGNATURES = {
                             _P, _P, _P, _F, _I, _P, _I, _I, _P, _SZ, _P]),
     "gpsig_sig_diag": (_I, [_P, _I, _I, _I, _I, _I, _I, _I, _F, _I, _P, _P, _SZ, _P]),
     "gpsig_sig_gram_vjp": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _I,
-                                _P, _P, _P, _F, _P, _P, _P, _P, _P, _P, _SZ, _P]),
+                                _P, _P, _P, _F, _P, _P, _P, _P, _P, _P, _P, _SZ, _P]),
+    "gpsig_sig_state_bytes": (_SZ, [_I, _I, _I, _I, _I]),
+    "gpsig_sig_gram_state": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _F, _I, _P,
+                                  _I, _I, _P, _SZ, _P, _SZ, _P]),
     "gpsig_pde_gram": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _I, _I, _P]),
     "gpsig_pde_diag": (_I, [_P, _I, _I, _I, _I, _I, _P, _P]),
     "gpsig_pde_vjp_workspace_bytes": (_SZ, [_I, _I, _I, _I]),

@@ -9,16 +9,25 @@ is the fused Gram kernel and the backward is the gpsig_sig_gram_vjp kernel (gpsi
     dLoss/ds; dLoss/drs is chained through rs = (K_m(a, a) + jitter)^-1/2 into one VJP launch over the
     diagonal pairs.
 
+When a gradient is needed, the forward Gram launch also saves its end-of-sweep state
+(gpsig_sig_gram_state: (M-1)(L2-1) + M floats per pair) and the VJP launch skips its own forward
+sweep; above GRAM_STATE_BYTES (env GPSIG_GRAM_STATE_BYTES) the VJP recomputes it instead.
+
 Gradients reach the sequences (and, through the host-side scaling in kernels.py, the lengthscales)
 and sigma * variances.  Supported for order == 1 with difference == True (the reference defaults);
 other configurations evaluate forward but raise NotImplementedError on backward.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 
 from . import _lib as L
 from . import ops
+
+
+GRAM_STATE_BYTES = int(os.environ.get("GPSIG_GRAM_STATE_BYTES", 16 << 30))
 
 
 def _check_bwd(cfg):
@@ -41,8 +50,15 @@ class SigGram(torch.autograd.Function):
             rs1 = ops.sig_diag(Xs.detach(), M, jitter=cfg["jitter"], rsqrt=True, **kw)
             rs2 = rs1 if X2s is None else ops.sig_diag(X2s.detach(), M, jitter=cfg["jitter"], rsqrt=True, **kw)
         jit = cfg["jitter"] if (cfg["normalization"] and X2s is None) else 0.0
+        state = None
+        if any(ctx.needs_input_grad[:3]) and cfg["order"] == 1 and cfg["difference"]:
+            n2 = None if X2s is None else X2s.shape[0]
+            numel = ops.sig_state_numel(Xs.shape[0], n2, Xs.shape[1] if X2s is None else X2s.shape[1], M)
+            if 0 < numel * 4 <= GRAM_STATE_BYTES:
+                state = torch.empty(numel, dtype=torch.float32, device=Xs.device)
         out = ops.sig_gram(Xs.detach(), None if X2s is None else X2s.detach(), M, rs1=rs1, rs2=rs2, scale=sc32,
-                           jitter=jit, out_mode=mode, **kw)
+                           jitter=jit, out_mode=mode, state=state, **kw)
+        ctx.state = state
         ctx.cfg = cfg
         ctx.scale_dtype = scale.dtype
         ctx.save_for_backward(Xs, X2s, sc32, rs1, rs2)
@@ -66,7 +82,8 @@ class SigGram(torch.autograd.Function):
         jit = cfg["jitter"] if (cfg["normalization"] and sym) else 0.0
         gX, gY = ops.sig_gram_vjp(Xs.detach(), None if sym else X2s.detach(), M, gout, base=cfg["base"],
                                   gout_levels=cfg["return_levels"], rs1=rs1, rs2=rs2, scale=sc32, jitter=jit,
-                                  grs1=grs1, grs2=grs2, gscale=gscale)
+                                  grs1=grs1, grs2=grs2, gscale=gscale, state=ctx.state)
+        ctx.state = None
         if cfg["normalization"]:
             # rs = (K_m(a, a) + jitter)^-1/2  ->  dLoss/dK_m(a, a) = -rs^3/2 dLoss/drs
             ops.sig_gram_vjp(Xs.detach(), None, M, grs1 * (-0.5) * rs1 ** 3, base=cfg["base"], diag=True, gX=gX)

@@ -48,11 +48,11 @@ extern "C" size_t gpsig_sig_workspace_bytes(int n1, int l1, int n2, int l2, int 
 
 static inline long long upper_prefix(long long r, long long ntb, long long k) { return r * ntb - k * r * (r - 1) / 2; }
 
-extern "C" int gpsig_sig_gram(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int num_levels,
-                              int order, int base_kind, int difference, int pair_mode, int row_begin, int row_end,
-                              const float *rs1, const float *rs2, const float *scale, float jitter, int out_mode,
-                              float *out, int out_row0, int out_rows, void *workspace, size_t workspace_bytes,
-                              gpsig_stream_t stream) {
+static int sig_gram_impl(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int num_levels,
+                         int order, int base_kind, int difference, int pair_mode, int row_begin, int row_end,
+                         const float *rs1, const float *rs2, const float *scale, float jitter, int out_mode,
+                         float *out, int out_row0, int out_rows, float *state, void *workspace,
+                         size_t workspace_bytes, gpsig_stream_t stream) {
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (!X || !Y || !out || n1 <= 0 || n2 <= 0 || d <= 0 || num_levels < 1) return GPSIG_EINVAL;
   if (l1 < 1 || l2 < 1 || (difference && (l1 < 2 || l2 < 2))) return GPSIG_EINVAL;
@@ -96,6 +96,7 @@ extern "C" int gpsig_sig_gram(const float *X, int n1, int l1, const float *Y, in
   a.out_rows = out_rows;
   a.out_ld = n2;
   a.out_lvl = (long long)out_rows * n2;
+  a.state = state;
 
   const int LP = (order == 1) ? fo_lanes_per_pair(l2, DP, num_levels) : ho_lanes_per_pair(l2, order, num_levels);
   if (LP == 0) return GPSIG_EUNSUPPORTED;
@@ -119,6 +120,41 @@ extern "C" int gpsig_sig_gram(const float *X, int n1, int l1, const float *Y, in
   }
   if (nblocks > 0x7fffffffLL) return GPSIG_EUNSUPPORTED;
   return (order == 1) ? sig_fo_launch(a, DP, seed, nblocks, s) : sig_ho_launch(a, DP, seed, nblocks, s);
+}
+
+extern "C" int gpsig_sig_gram(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int num_levels,
+                              int order, int base_kind, int difference, int pair_mode, int row_begin, int row_end,
+                              const float *rs1, const float *rs2, const float *scale, float jitter, int out_mode,
+                              float *out, int out_row0, int out_rows, void *workspace, size_t workspace_bytes,
+                              gpsig_stream_t stream) {
+  return sig_gram_impl(X, n1, l1, Y, n2, l2, d, num_levels, order, base_kind, difference, pair_mode, row_begin,
+                       row_end, rs1, rs2, scale, jitter, out_mode, out, out_row0, out_rows, nullptr, workspace,
+                       workspace_bytes, stream);
+}
+
+extern "C" size_t gpsig_sig_state_bytes(int n1, int n2, int l2, int num_levels, int pair_mode) {
+  if (n1 <= 0 || n2 <= 0 || l2 < 2 || num_levels < 1) return 0;
+  long long slots;
+  if (pair_mode == GPSIG_PAIRS_RECT) slots = (long long)n1 * n2;
+  else if (pair_mode == GPSIG_PAIRS_UPPER && n1 == n2) slots = (long long)n1 * (n1 + 1) / 2;
+  else return 0;
+  return (size_t)slots * (size_t)state_stride(num_levels, l2) * sizeof(float);
+}
+
+extern "C" int gpsig_sig_gram_state(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d,
+                                    int num_levels, int base_kind, int pair_mode, int row_begin, int row_end,
+                                    const float *rs1, const float *rs2, const float *scale, float jitter,
+                                    int out_mode, float *out, int out_row0, int out_rows, float *state,
+                                    size_t state_bytes, void *workspace, size_t workspace_bytes,
+                                    gpsig_stream_t stream) {
+  if (!state) return GPSIG_EINVAL;
+  if (pair_mode != GPSIG_PAIRS_RECT && pair_mode != GPSIG_PAIRS_UPPER) return GPSIG_EINVAL;
+  const size_t need = gpsig_sig_state_bytes(n1, n2, l2, num_levels, pair_mode);
+  if (need == 0) return GPSIG_EINVAL;
+  if (state_bytes < need) return GPSIG_EWORKSPACE;
+  return sig_gram_impl(X, n1, l1, Y, n2, l2, d, num_levels, 1, base_kind, 1, pair_mode, row_begin, row_end, rs1,
+                       rs2, scale, jitter, out_mode, out, out_row0, out_rows, state, workspace, workspace_bytes,
+                       stream);
 }
 
 extern "C" int gpsig_sig_diag(const float *X, int n, int l, int d, int num_levels, int order, int base_kind,

@@ -87,6 +87,12 @@ GPSIG_DEV float group_sum(float v) {
 
 GPSIG_DEV int wave_uniform(int v) { return __builtin_amdgcn_readfirstlane(v); }
 
+// Read-only view of data no launch in flight writes (feature records): loads through the constant
+// address space may use the scalar unit even when the kernel also stores or issues atomics, which
+// would otherwise keep wave-uniform global loads on the vector path (behind the atomics in vmcnt).
+using cfloat = const __attribute__((address_space(4))) float;
+GPSIG_DEV cfloat *as_const(const float *p) { return (cfloat *)p; }
+
 // ---------------------------------------------------------------------------------------------
 // expm1 on |x| <= 0.5 as x * P5(x): minimax (Lawson) fit of expm1(x)/x on [-0.5, 0.5], max
 // relative error 2.2e-7 in fp32 with FMA Horner (tests/test_numerics.py pins it).  Only used where

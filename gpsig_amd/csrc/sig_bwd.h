@@ -40,6 +40,7 @@ struct BwdArgs {
   const float *rs1, *rs2, *scale;
   float jitter;
   float *gX, *gY, *grs1, *grs2, *gscale;
+  const float *state;  // optional saved forward state (RECT / UPPER), see gpsig_sig_gram_state
 };
 
 // Exclusive scan over the group's columns of per-lane column arrays v[W] (W columns of lane gl hold
@@ -143,6 +144,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
   const int l1 = p.l1, l2 = p.l2;
 
   const float *__restrict__ fx = p.FX + (long long)a * l1 * FS;
+  cfloat *fxc = as_const(fx);  // row records: scalar loads, independent of the atomics below
   const float *__restrict__ fy = p.FY + (long long)bl * l2 * FS;
 
   // ---- column data of this lane
@@ -164,7 +166,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
   }
 
   // k(x_i, y_j) of one point row (RBF); identical instructions in both sweeps
-  auto krow = [&](const float *__restrict__ xr, float (&k)[W]) {
+  auto krow = [&](cfloat *xr, float (&k)[W]) {
 #pragma unroll
     for (int w = 0; w < W; ++w) {
       float s = 0.0f;
@@ -177,7 +179,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
     }
   };
   // cells dM(i, j) of row i from k rows i (kc) and i+1 (kn); kcR/knR = right neighbour of column W-1
-  auto cells = [&](const float *__restrict__ fr, const float (&kc)[W], const float (&kn)[W], float kcR, float knR,
+  auto cells = [&](cfloat *fr, const float (&kc)[W], const float (&kn)[W], float kcR, float knR,
                    float (&dM)[W]) {
     if constexpr (RBF) {
       const float hdx = fr[2 * DP];
@@ -212,58 +214,79 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
     }
   };
 
-  // ---- forward sweep
+  // ---- forward sweep, or its end state saved by the forward launch (gpsig_sig_gram_state)
   float C[M][W];
 #pragma unroll
   for (int m = 0; m < M; ++m)
 #pragma unroll
     for (int w = 0; w < W; ++w) C[m][w] = 0.0f;
   float kc[W], kcR = 0.0f;
-  if constexpr (RBF) {
-    krow(fx, kc);
-    kcR = lane_next(kc[0]);
-  }
+  float K[M + 1];
+  K[0] = 1.0f;
   const int nrows = l1 - 1;
-  for (int i = 0; i < nrows; ++i) {
-    const float *__restrict__ fr = fx + (long long)i * FS;
-    float kn[W], knR = 0.0f, dM[W];
+  const bool saved = p.state != nullptr;  // kernel-uniform
+  if (saved) {
+    const int nc = l2 - 1;
+    const float *__restrict__ st =
+        p.state + (pair_ok ? state_slot(a, bl, p.n2, p.pair_mode == GPSIG_PAIRS_UPPER) * state_stride(M, l2) : 0);
+#pragma unroll
+    for (int m = 0; m + 1 < M; ++m)
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        const int j = gl * W + w;
+        C[m][w] = (pair_ok && j < nc) ? st[(long long)m * nc + j] : 0.0f;
+      }
+#pragma unroll
+    for (int m = 1; m <= M; ++m) K[m] = pair_ok ? st[(long long)(M - 1) * nc + m - 1] : 0.0f;
     if constexpr (RBF) {
-      krow(fr + FS, kn);
-      knR = lane_next(kn[0]);
+      krow(fxc + (long long)nrows * FS, kc);  // k row of the last point, as the sweep would leave it
+      kcR = lane_next(kc[0]);
     }
-    cells(fr, kc, kn, kcR, knR, dM);
-    if constexpr (M > 1) {
-      float Cs[ML][W], S[ML][W];
-#pragma unroll
-      for (int m = 0; m < ML; ++m)
-#pragma unroll
-        for (int w = 0; w < W; ++w) Cs[m][w] = C[m][w];
-      group_excl_cols_n<LP, W, ML>(Cs, S);
-#pragma unroll
-      for (int m = 1; m < M; ++m)
-#pragma unroll
-        for (int w = 0; w < W; ++w) C[m][w] = __builtin_fmaf(dM[w], S[m - 1][w], C[m][w]);
-    }
-#pragma unroll
-    for (int w = 0; w < W; ++w) C[0][w] += dM[w];
+  } else {
     if constexpr (RBF) {
-#pragma unroll
-      for (int w = 0; w < W; ++w) kc[w] = kn[w];
-      kcR = knR;
+      krow(fxc, kc);
+      kcR = lane_next(kc[0]);
     }
+    for (int i = 0; i < nrows; ++i) {
+      cfloat *fr = fxc + (long long)i * FS;
+      float kn[W], knR = 0.0f, dM[W];
+      if constexpr (RBF) {
+        krow(fr + FS, kn);
+        knR = lane_next(kn[0]);
+      }
+      cells(fr, kc, kn, kcR, knR, dM);
+      if constexpr (M > 1) {
+        float Cs[ML][W], S[ML][W];
+#pragma unroll
+        for (int m = 0; m < ML; ++m)
+#pragma unroll
+          for (int w = 0; w < W; ++w) Cs[m][w] = C[m][w];
+        group_excl_cols_n<LP, W, ML>(Cs, S);
+#pragma unroll
+        for (int m = 1; m < M; ++m)
+#pragma unroll
+          for (int w = 0; w < W; ++w) C[m][w] = __builtin_fmaf(dM[w], S[m - 1][w], C[m][w]);
+      }
+#pragma unroll
+      for (int w = 0; w < W; ++w) C[0][w] += dM[w];
+      if constexpr (RBF) {
+#pragma unroll
+        for (int w = 0; w < W; ++w) kc[w] = kn[w];
+        kcR = knR;
+      }
+    }
+
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      float s = 0.0f;
+#pragma unroll
+      for (int w = 0; w < W; ++w) s += C[m][w];
+      K[m + 1] = group_sum<LP>(s);
+    }
+    K[1] = level1_closed<DP, SEED>(fx, fy, l1, l2);
   }
 
   // ---- per-level weights g_m = dLoss/dK_m(a, b) and the normalisation / scale terms
-  float K[M + 1];
-  K[0] = 1.0f;
-#pragma unroll
-  for (int m = 0; m < M; ++m) {
-    float s = 0.0f;
-#pragma unroll
-    for (int w = 0; w < W; ++w) s += C[m][w];
-    K[m + 1] = group_sum<LP>(s);
-  }
-  K[1] = level1_closed<DP, SEED>(fx, fy, l1, l2);
 
   float gw[M + 1];
   {
@@ -329,7 +352,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
   // point row `pi` of the grid receives dLoss/dk(x_pi, y_j) = Kh[w]: x-gradient reduced over the wave
   // (all pairs of a wave share a), y-gradient accumulated per column
   auto emit = [&](int pi, const float (&Kh)[W], const float (&kr)[W]) {
-    const float *__restrict__ xp = fx + (long long)pi * FS;
+    cfloat *xp = fxc + (long long)pi * FS;
     float xi[DP];
 #pragma unroll
     for (int k = 0; k < DP; ++k) xi[k] = xp[k];
@@ -371,7 +394,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
     for (int w = 0; w < W; ++w) kr1[w] = 1.0f;
   }
   for (int i = nrows - 1; i >= 0; --i) {
-    const float *__restrict__ fr = fx + (long long)i * FS;
+    cfloat *fr = fxc + (long long)i * FS;
     float k0[W], k0R = 0.0f, dM[W];
     if constexpr (RBF) {
       krow(fr, k0);

@@ -42,7 +42,8 @@ extern "C" int gpsig_sig_gram_vjp(const float *X, int n1, int l1, const float *Y
                                   int num_levels, int base_kind, int pair_mode, int row_begin, int row_end,
                                   const float *gout, int gout_levels, const float *rs1, const float *rs2,
                                   const float *scale, float jitter, float *gX, float *gY, float *grs1, float *grs2,
-                                  float *gscale, void *workspace, size_t workspace_bytes, gpsig_stream_t stream) {
+                                  float *gscale, const float *state, void *workspace, size_t workspace_bytes,
+                                  gpsig_stream_t stream) {
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (!X || !Y || !gout || !gX || n1 <= 0 || n2 <= 0 || d <= 0 || num_levels < 1) return GPSIG_EINVAL;
   if (l1 < 2 || l2 < 2) return GPSIG_EINVAL;
@@ -52,6 +53,7 @@ extern "C" int gpsig_sig_gram_vjp(const float *X, int n1, int l1, const float *Y
   if (pair_mode == GPSIG_PAIRS_RECT && !gY) return GPSIG_EINVAL;
   if (pair_mode == GPSIG_PAIRS_DIAG && !gout_levels) return GPSIG_EINVAL;
   if ((rs1 == nullptr) != (rs2 == nullptr)) return GPSIG_EINVAL;
+  if (state && pair_mode == GPSIG_PAIRS_DIAG) return GPSIG_EINVAL;
   const int seed = base_kind == GPSIG_BASE_RBF ? SEED_RBF_DIFF : (base_kind == GPSIG_BASE_LINEAR ? SEED_LIN_DIFF : -1);
   const int DP = bwd_pad(d);
   if (seed < 0 || DP == 0) return GPSIG_EUNSUPPORTED;
@@ -88,6 +90,7 @@ extern "C" int gpsig_sig_gram_vjp(const float *X, int n1, int l1, const float *Y
   a.grs1 = grs1;
   a.grs2 = pair_mode == GPSIG_PAIRS_RECT ? grs2 : grs1;
   a.gscale = gscale;
+  a.state = state;
 
   const int G = 64 / geo.LP;
   long long nblocks;

@@ -34,7 +34,15 @@ struct SigArgs {
   float *out;
   int out_row0, out_rows;
   long long out_ld, out_lvl;  // row stride, level stride (elements)
+  float *state;               // optional saved forward state for the VJP (gpsig_sig_gram_state)
 };
+
+// Saved forward state of a first-order pair (gpsig_sig_gram_state): column sums of levels 1..M-1
+// after the last row ((M-1) x (l2-1) floats, level-major), then the raw levels K_1..K_M.
+__host__ __device__ inline long long state_stride(int M, int l2) { return (long long)(M - 1) * (l2 - 1) + M; }
+__host__ __device__ inline long long state_slot(int a, int b, int n2, bool upper) {
+  return upper ? (long long)a * n2 - (long long)a * (a - 1) / 2 + (b - a) : (long long)a * n2 + b;
+}
 
 // Wave-uniform record of row i: x_{i+1} (RBF DIFF) or x_i (POINT seeds), dx_i, |dx_i|^2/2.
 template <int DP>

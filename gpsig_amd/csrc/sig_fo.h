@@ -162,6 +162,24 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
     if constexpr (Seed::DIFF) K[1] = level1_closed<DP, SEED>(fx, fy, p.l1, p.l2);
     store_pair<M>(p, a, b, K);
   }
+  if constexpr (!DIAGK && Seed::DIFF) {
+    if (p.state && pair_ok) {  // end-of-sweep state for the VJP (column pair k = columns k, k + W/2)
+      const int nc = p.l2 - 1;
+      float *__restrict__ st = p.state + state_slot(a, b, p.n2, p.pair_mode == GPSIG_PAIRS_UPPER) * state_stride(M, p.l2);
+#pragma unroll
+      for (int m = 0; m + 1 < M; ++m)
+#pragma unroll
+        for (int w2 = 0; w2 < W2; ++w2)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int j = gl * W + w2 + h * W2;
+            if (j < nc) st[(long long)m * nc + j] = C[m][w2][h];
+          }
+      if (gl == 0)
+#pragma unroll
+        for (int m = 1; m <= M; ++m) st[(long long)(M - 1) * nc + m - 1] = K[m];
+    }
+  }
 }
 
 // Column geometry: W columns per lane, LP lanes per pair; capacity LP*W >= points per sequence.

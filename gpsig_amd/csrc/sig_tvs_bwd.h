@@ -168,9 +168,10 @@ __device__ __forceinline__ void tvs_bwd_level(const TvsBwdArgs &a) {
     for (int q = 0; q < DP; ++q) V0[k][q] = V1[k][q] = 0.f;
   }
   // point s' receives dLoss/dP_k(s') = Ph for every component k (point values v0, v1 at s')
-  auto emit = [&](int sp, const float (&Ph)[LT], const float (&v0)[LT], const float (&v1)[LT]) {
-    float xp[DP];
-    ldx(sp, xp);
+  // (xp = x at s', kept from the sweep: no load here, so the atomics below never sit in front of a
+  // load the next step waits for)
+  auto emit = [&](int sp, const float (&Ph)[LT], const float (&v0)[LT], const float (&v1)[LT],
+                  const float (&xp)[DP]) {
     float gxa[DP], gxs = 0.f;
 #pragma unroll
     for (int q = 0; q < DP; ++q) gxa[q] = 0.f;
@@ -204,19 +205,28 @@ __device__ __forceinline__ void tvs_bwd_level(const TvsBwdArgs &a) {
       }
     }
     if (valid) {
-      for (int q = 0; q < d; ++q) {
+#pragma unroll
+      for (int q = 0; q < DP; ++q) {
         const float v = RBF ? __builtin_fmaf(-gxs, xp[q], gxa[q]) : gxa[q];
-        unsafeAtomicAdd(a.gXt + ((long long)sp * d + q) * n + s0, v);
+        if (q < d) unsafeAtomicAdd(a.gXt + ((long long)sp * d + q) * n + s0, v);
       }
     }
   };
 
-  for (int s = L - 2; s >= 0; --s) {
-    float x[DP], dx[DP];
-    ldx(s, x);
+  // row s of the reverse sweep is loaded one step ahead (before the previous step's atomics)
+  float xs1[DP], x[DP], dx[DP], gs;  // xs1 = x at s + 1
+  ldx(L - 1, xs1);
+  ldx(L - 2, x);
 #pragma unroll
-    for (int q = 0; q < DP; ++q) dx[q] = q < d ? ld(s, d + q) : 0.f;
-    const float gs = ld(s, 2 * d + 1);
+  for (int q = 0; q < DP; ++q) dx[q] = q < d ? ld(L - 2, d + q) : 0.f;
+  gs = ld(L - 2, 2 * d + 1);
+  for (int s = L - 2; s >= 0; --s) {
+    float xn[DP], dxn[DP], gsn = 0.f;  // row s - 1
+    const int sn = s > 0 ? s - 1 : 0;
+    ldx(sn, xn);
+#pragma unroll
+    for (int q = 0; q < DP; ++q) dxn[q] = q < d ? ld(sn, d + q) : 0.f;
+    gsn = ld(sn, 2 * d + 1);
     float c0[LT], c1[LT], Ph[LT];
     {
       constexpr int i = I, k0 = 0;
@@ -250,18 +260,25 @@ __device__ __forceinline__ void tvs_bwd_level(const TvsBwdArgs &a) {
         Acc[k0 + j - 1] = __builtin_fmaf(m[j], Qn, Acc[k0 + j - 1]);
       }
     }
-    emit(s + 1, Ph, pv0, pv1);
+    emit(s + 1, Ph, pv0, pv1, xs1);
 #pragma unroll
     for (int k = 0; k < LT; ++k) {
       pv0[k] = c0[k];
       pv1[k] = c1[k];
     }
+#pragma unroll
+    for (int q = 0; q < DP; ++q) {
+      xs1[q] = x[q];
+      x[q] = xn[q];
+      dx[q] = dxn[q];
+    }
+    gs = gsn;
   }
   {
     float Ph[LT];
 #pragma unroll
     for (int k = 0; k < LT; ++k) Ph[k] = -Mh[k];
-    emit(0, Ph, pv0, pv1);
+    emit(0, Ph, pv0, pv1, xs1);
   }
 
   // ---- tensor gradients: reduce over the wave's sequences, one atomic per component channel

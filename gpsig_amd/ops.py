@@ -76,12 +76,14 @@ def sig_diag(X: torch.Tensor, num_levels: int, order: int = 1, base="rbf", diffe
 def sig_gram(X: torch.Tensor, Y: torch.Tensor | None, num_levels: int, order: int = 1, base="rbf",
              difference: bool = True, rows: tuple | None = None, rs1=None, rs2=None, scale=None,
              jitter: float = 0.0, out_mode: int = L.OUT_LEVELS, out: torch.Tensor | None = None,
-             out_row0: int | None = None) -> torch.Tensor:
+             out_row0: int | None = None, state: torch.Tensor | None = None) -> torch.Tensor:
     """Signature-kernel Gram between the sequences of X (n1,l1,d) and Y (n2,l2,d).
 
     Y is None -> symmetric K(X): only b >= a is evaluated and mirrored.  rows=(r0, r1) restricts the
     evaluated rows (row sharding); the output then holds rows [out_row0, out_row0 + out.shape[-2]).
     out_mode: L.OUT_LEVELS (raw per level), L.OUT_NORM_LEVELS, L.OUT_NORM_SUM (fused normalisation).
+    state: float32 buffer of sig_state_numel(...) elements -> also save the VJP's forward state
+    (gpsig_sig_gram_state; order 1, difference=True).
     """
     _require_cuda(X, Y, rs1, rs2, scale)
     lib = L.load()
@@ -106,21 +108,43 @@ def sig_gram(X: torch.Tensor, Y: torch.Tensor | None, num_levels: int, order: in
         scale = _f32(scale)
     nb = lib.gpsig_sig_workspace_bytes(n1, l1, n2, l2, d)
     ws = workspace(X.device, nb)
+    pm = L.PAIRS_UPPER if sym else L.PAIRS_RECT
+    if state is not None:
+        if order != 1 or not difference:
+            raise ValueError("the saved VJP state needs order=1 and difference=True")
+        if state.dtype != torch.float32 or not state.is_contiguous() or state.device != X.device:
+            raise ValueError("state must be a contiguous float32 tensor on the input's device")
+        rc = lib.gpsig_sig_gram_state(X.data_ptr(), n1, l1, Y.data_ptr(), n2, l2, d, num_levels, base_kind(base),
+                                      pm, r0, r1, _ptr(rs1), _ptr(rs2), _ptr(scale), float(jitter), out_mode,
+                                      out.data_ptr(), out_row0, out_rows, state.data_ptr(), state.numel() * 4,
+                                      ws.data_ptr(), ws.numel(), _stream(X.device))
+        L.check(rc, "gpsig_sig_gram_state")
+        return out
     rc = lib.gpsig_sig_gram(X.data_ptr(), n1, l1, Y.data_ptr(), n2, l2, d, num_levels, order, base_kind(base),
-                            int(difference), L.PAIRS_UPPER if sym else L.PAIRS_RECT, r0, r1,
+                            int(difference), pm, r0, r1,
                             _ptr(rs1), _ptr(rs2), _ptr(scale), float(jitter), out_mode, out.data_ptr(),
                             out_row0, out_rows, ws.data_ptr(), ws.numel(), _stream(X.device))
     L.check(rc, "gpsig_sig_gram")
     return out
 
 
+def sig_state_numel(n1: int, n2: int | None, l2: int, num_levels: int) -> int:
+    """float32 elements of the saved VJP state of a Gram call (n2 None: symmetric K(X), upper
+    triangle)."""
+    lib = L.load()
+    sym = n2 is None
+    nb = lib.gpsig_sig_state_bytes(n1, n1 if sym else n2, l2, num_levels, L.PAIRS_UPPER if sym else L.PAIRS_RECT)
+    return nb // 4
+
+
 def sig_gram_vjp(X: torch.Tensor, Y: torch.Tensor | None, num_levels: int, gout: torch.Tensor, base="rbf",
                  gout_levels: bool = False, diag: bool = False, rs1=None, rs2=None, scale=None, jitter: float = 0.0,
                  gX: torch.Tensor | None = None, gY: torch.Tensor | None = None, grs1=None, grs2=None,
-                 gscale=None, rows: tuple | None = None):
+                 gscale=None, rows: tuple | None = None, state: torch.Tensor | None = None):
     """dLoss/dX (and dLoss/dY, dLoss/drs, dLoss/dscale) of the first-order Gram, accumulated into float32
     buffers: see gpsig_sig_gram_vjp in include/gpsig_amd.h.  Y None -> symmetric K(X) (or the diagonal
-    with diag=True; gout is then (num_levels+1, n) per level).  Returns (gX, gY)."""
+    with diag=True; gout is then (num_levels+1, n) per level).  state: the buffer a sig_gram(...,
+    state=) call on the same inputs filled -> the forward sweep is skipped.  Returns (gX, gY)."""
     _require_cuda(X, Y, gout, rs1, rs2, scale)
     lib = L.load()
     X = _f32(X)
@@ -142,6 +166,8 @@ def sig_gram_vjp(X: torch.Tensor, Y: torch.Tensor | None, num_levels: int, gout:
         if tuple(gout.shape) != want:
             raise ValueError(f"gout must have shape {want}, got {tuple(gout.shape)}")
     r0, r1 = (0, n1) if rows is None else rows
+    if state is not None and diag:
+        raise ValueError("the saved state is for Gram (RECT / UPPER) calls, not diag=True")
     if gX is None:
         gX = torch.zeros((n1, l1, d), dtype=torch.float32, device=X.device)
     if not sym and gY is None:
@@ -159,7 +185,7 @@ def sig_gram_vjp(X: torch.Tensor, Y: torch.Tensor | None, num_levels: int, gout:
     rc = lib.gpsig_sig_gram_vjp(X.data_ptr(), n1, l1, Y.data_ptr(), n2, l2, d, num_levels, base_kind(base), mode, r0, r1,
                                 gout.data_ptr(), int(bool(gout_levels)), _ptr(rs1), _ptr(rs2), _ptr(scale),
                                 float(jitter), gX.data_ptr(), _ptr(gY), _ptr(grs1), _ptr(grs2), _ptr(gscale),
-                                ws.data_ptr(), ws.numel(), _stream(X.device))
+                                _ptr(state), ws.data_ptr(), ws.numel(), _stream(X.device))
     L.check(rc, "gpsig_sig_gram_vjp")
     return gX, gY
 

@@ -83,6 +83,20 @@ int gpsig_sig_gram(const float *X, int n1, int l1, const float *Y, int n2, int l
                    float *out, int out_row0, int out_rows, void *workspace, size_t workspace_bytes,
                    gpsig_stream_t stream);
 
+/* Training variant of gpsig_sig_gram: also saves, per evaluated pair (a, b), the forward state the
+ * VJP would otherwise recompute -- the column sums C_m(L1-1, j) of levels 1..L-1 at the end of the row
+ * sweep (j < l2-1) and the raw levels K_1..K_L -- so that gpsig_sig_gram_vjp given the same `state`
+ * skips its forward sweep.  The reference keeps every (N1, L1, N2, L2) intermediate of the TF graph
+ * alive for autodiff (kernels.py:209-238); this keeps (L-1)(l2-1) + L floats per pair.
+ * Pair slot: RECT a*n2 + b; UPPER the row-major upper triangle a*n2 - a(a-1)/2 + (b - a).
+ * order == 1, difference == 1, pair_mode RECT or UPPER; state_bytes >= gpsig_sig_state_bytes(...). */
+size_t gpsig_sig_state_bytes(int n1, int n2, int l2, int num_levels, int pair_mode);
+int gpsig_sig_gram_state(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int num_levels,
+                         int base_kind, int pair_mode, int row_begin, int row_end, const float *rs1,
+                         const float *rs2, const float *scale, float jitter, int out_mode, float *out,
+                         int out_row0, int out_rows, float *state, size_t state_bytes, void *workspace,
+                         size_t workspace_bytes, gpsig_stream_t stream);
+
 /* Diagonal k(x_a, x_a) per level: _K_seq_diag (kernels.py:190-207).  out_mode LEVELS or RSQRT. */
 int gpsig_sig_diag(const float *X, int n, int l, int d, int num_levels, int order, int base_kind, int difference,
                    float jitter, int out_mode, float *out, void *workspace, size_t workspace_bytes,
@@ -103,13 +117,14 @@ int gpsig_sig_diag(const float *X, int n, int l, int d, int num_levels, int orde
  *   gX (n1, l1, d) and gY (n2, l2, d) (UPPER / DIAG: Y == X and everything goes to gX);
  *   grs1 (L+1, n1), grs2 (L+1, n2) = dLoss/drs (the host chains them through rs = (diag+jitter)^-1/2
  *   into a DIAG call); gscale (L+1) = dLoss/dscale.  Any of grs1/grs2/gscale may be NULL.
+ *   state: NULL, or the buffer a gpsig_sig_gram_state call with the same inputs filled (RECT/UPPER).
  *   Workspace: gpsig_sig_workspace_bytes(n1, l1, n2, l2, d).
  */
 int gpsig_sig_gram_vjp(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int num_levels,
                        int base_kind, int pair_mode, int row_begin, int row_end, const float *gout, int gout_levels,
                        const float *rs1, const float *rs2, const float *scale, float jitter, float *gX, float *gY,
-                       float *grs1, float *grs2, float *gscale, void *workspace, size_t workspace_bytes,
-                       gpsig_stream_t stream);
+                       float *grs1, float *grs2, float *gscale, const float *state, void *workspace,
+                       size_t workspace_bytes, gpsig_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Inducing tensors (sparse rank-1 tensors z = (z_{m,1} (x) ... (x) z_{m,m})_m).

@@ -149,6 +149,58 @@ def test_raw_levels_vjp_ragged_lengths(base):
 
 
 @pytest.mark.parametrize("base", ["rbf", "linear"])
+@pytest.mark.parametrize("sym", [False, True])
+@pytest.mark.parametrize("D,M,L1,L2", [(5, 5, 100, 100), (3, 4, 19, 45), (8, 6, 33, 128), (2, 2, 64, 7)])
+def test_saved_state_vjp(base, sym, D, M, L1, L2):
+    """The VJP from the forward launch's saved end state (gpsig_sig_gram_state) equals the VJP that
+    recomputes its forward sweep, and the fp64 autodiff gradient; the forward output is unchanged."""
+    from gpsig_amd import ops
+    if sym:
+        L2 = L1
+    N1, N2 = 9, 7
+    X = torch.tensor(walks(N1, L1, D, 20), device=DEV)
+    Y = None if sym else torch.tensor(walks(N2, L2, D, 21), device=DEV)
+    n2 = N1 if sym else N2
+    G = torch.tensor(np.random.default_rng(22).standard_normal((M + 1, N1, n2)), device=DEV)
+    if sym:
+        G = G + G.transpose(1, 2)
+    st = torch.empty(ops.sig_state_numel(N1, None if sym else N2, L2, M), dtype=torch.float32, device=DEV)
+    K0 = ops.sig_gram(X, Y, M, base=base)
+    K1 = ops.sig_gram(X, Y, M, base=base, state=st)
+    assert torch.equal(K0, K1)
+    g0 = ops.sig_gram_vjp(X, Y, M, G, base=base, gout_levels=True)
+    g1 = ops.sig_gram_vjp(X, Y, M, G, base=base, gout_levels=True, state=st)
+    Xr = torch.tensor(X.cpu().numpy().astype(np.float64), requires_grad=True)
+    Yr = None if sym else torch.tensor(Y.cpu().numpy().astype(np.float64), requires_grad=True)
+    Gr = G.cpu().double()
+    if sym:  # K(X) evaluates the upper triangle and mirrors: dK(a,b) and dK(b,a) both flow to the pair
+        (ar.k_seq(Xr, Xr, M, base) * Gr).sum().backward()
+    else:
+        (ar.k_seq(Xr, Yr, M, base) * Gr).sum().backward()
+    assert norm_rel_err(g1[0].cpu().numpy(), g0[0].cpu().numpy()) < 1e-5
+    assert norm_rel_err(g1[0].cpu().numpy(), Xr.grad.numpy()) < GTOL
+    if not sym:
+        assert norm_rel_err(g1[1].cpu().numpy(), g0[1].cpu().numpy()) < 1e-5
+        assert norm_rel_err(g1[1].cpu().numpy(), Yr.grad.numpy()) < GTOL
+
+
+def test_autograd_state_budget(monkeypatch):
+    """K(X).backward with the saved state and with the recompute fallback (budget 0) agree."""
+    import gpsig_amd
+    import gpsig_amd.autograd as ag
+    N, L, D, M = 10, 40, 4, 4
+    X = walks(N, L, D, 30)
+    G = np.random.default_rng(31).standard_normal((N, N))
+    k = gpsig_amd.SignatureRBF(L * D, D, M)
+    a, _ = grads_gpu(k, X, None, G)
+    monkeypatch.setattr(ag, "GRAM_STATE_BYTES", 0)
+    b, _ = grads_gpu(k, X, None, G)
+    ref, _, _, _ = grads_ref(X, None, G, M)
+    assert norm_rel_err(a[0], b[0]) < 1e-5
+    assert norm_rel_err(a[0], ref[0]) < GTOL
+
+
+@pytest.mark.parametrize("base", ["rbf", "linear"])
 @pytest.mark.parametrize("increments", [False, True])
 @pytest.mark.parametrize("M,D,L", [(3, 3, 20), (5, 5, 40), (1, 2, 9), (8, 8, 12)])
 def test_tens_vs_seq_vjp_matches_autodiff(base, increments, M, D, L):
