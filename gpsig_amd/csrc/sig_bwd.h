@@ -109,6 +109,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
   constexpr int G = 64 / LP;
   constexpr bool RBF = (SEED == SEED_RBF_DIFF);
   constexpr float NHL2E = -0.72134752044448170f;  // exp(-d2/2) = exp2(d2 * NHL2E)
+  constexpr float L2E = 1.4426950408889634f;
+  constexpr int RC = W >= 4 ? 4 : 8;  // rows per chunk of the reverse sweep (<= the forward's anchor period)
+  __shared__ __attribute__((aligned(16))) float cbuf[RBF ? 4 : 1][RBF ? RC : 1][64][2 * W];
   constexpr int ML = M > 1 ? M - 1 : 1;
 
   const int lane = threadIdx.x & 63;
@@ -384,27 +387,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
     }
   };
 
-  float kr1[W], kr1R = 0.0f;  // k row i+1
+  float kr1[W];  // k row of point i+1
   if constexpr (RBF) {
 #pragma unroll
     for (int w = 0; w < W; ++w) kr1[w] = kc[w];
-    kr1R = kcR;
   } else {
 #pragma unroll
     for (int w = 0; w < W; ++w) kr1[w] = 1.0f;
   }
-  for (int i = nrows - 1; i >= 0; --i) {
-    cfloat *fr = fxc + (long long)i * FS;
-    float k0[W], k0R = 0.0f, dM[W];
-    if constexpr (RBF) {
-      krow(fr, k0);
-      k0R = lane_next(k0[0]);
-    } else {
-#pragma unroll
-      for (int w = 0; w < W; ++w) k0[w] = 1.0f;
-    }
-    cells(fr, k0, kr1, k0R, kr1R, dM);
-
+  // one row of the reverse sweep from its cells dM(i, .) and the k row of point i
+  auto rev_row = [&](int i, const float (&dM)[W], const float (&k0)[W]) {
     // forward state of row i: C_m(i) = C_m(i+1) - dM S_{m-1}(i), ascending levels (C[m] holds level m+1,
     // S_0 = 1), and dLoss/d dM(i, j) = sum_m Ch_m(i+1, j) S_{m-1}(i, j)
     float Dh[W];
@@ -456,7 +448,100 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
     emit(i + 1, Kh, kr1);
 #pragma unroll
     for (int w = 0; w < W; ++w) kr1[w] = k0[w];
-    kr1R = k0R;
+  };
+
+  if constexpr (RBF) {
+    // Chunked: the cells of RC rows are regenerated forward from an exact row (k and expm1(q) from
+    // x - y) with the exp-free recurrences of the forward kernel (sig_common.h RbfSeedPk; chunk
+    // starts at multiples of RC <= its anchor period, so the cells are the forward launch's) into
+    // this lane's LDS slots, then consumed in reverse.  Cells with |p| or |c| >= EM1_TAU take the
+    // corner difference of the k grid with an exact next row (wave-uniform branch).
+    float(*cb)[64][2 * W] = cbuf[wave];
+    auto exact_row = [&](cfloat *xr, float (&k)[W], float (&Eq)[W]) {
+      float xv[DP];
+#pragma unroll
+      for (int c = 0; c < DP; ++c) xv[c] = xr[c];
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        float s2 = 0.0f, q = -hdy[w];
+#pragma unroll
+        for (int c = 0; c < DP; ++c) {
+          const float df = xv[c] - y[w][c];
+          s2 = __builtin_fmaf(df, df, s2);
+          q = __builtin_fmaf(df, dy[w][c], q);
+        }
+        k[w] = __builtin_amdgcn_exp2f(s2 * NHL2E);
+        Eq[w] = __builtin_fabsf(q) < EM1_TAU ? em1_small(q) : __builtin_amdgcn_exp2f(q * L2E) - 1.0f;
+      }
+    };
+    auto chunk_fwd = [&](int i0, int nr) {
+      float kc[W], Eq[W];
+      exact_row(fxc + (long long)i0 * FS, kc, Eq);
+      for (int r = 0; r < nr; ++r) {
+        cfloat *fr = fxc + (long long)(i0 + r) * FS;
+        float dxv[DP];
+#pragma unroll
+        for (int c = 0; c < DP; ++c) dxv[c] = fr[DP + c];
+        const float g = fr[2 * DP + 1];
+        float dM[W], kn[W], Eqn[W], mx[W];
+        bool slow = false;
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          float pp = -g, c = 0.0f;
+#pragma unroll
+          for (int k = 0; k < DP; ++k) {
+            pp = __builtin_fmaf(y[w][k], dxv[k], pp);
+            c = __builtin_fmaf(dy[w][k], dxv[k], c);
+          }
+          const float Ep = em1_small(pp), Ec = em1_small(c);
+          float t = __builtin_fmaf(Ep, Ec, Ec);
+          t = __builtin_fmaf(Eq[w], t, t);
+          dM[w] = kc[w] * __builtin_fmaf(Ep, Eq[w], t);
+          kn[w] = __builtin_fmaf(kc[w], Ep, kc[w]);
+          Eqn[w] = __builtin_fmaf(Eq[w], Ec, Eq[w] + Ec);
+          mx[w] = __builtin_fmaxf(__builtin_fabsf(pp), __builtin_fabsf(c));
+          slow = slow || !(mx[w] < EM1_TAU);
+        }
+        if (__builtin_amdgcn_ballot_w64(slow) != 0) {
+          exact_row(fr + FS, kn, Eqn);
+          const float knR = lane_next(kn[0]), kcR2 = lane_next(kc[0]);
+#pragma unroll
+          for (int w = 0; w < W; ++w) {
+            const float kn1 = (w + 1 < W) ? kn[w + 1] : knR;
+            const float kc1 = (w + 1 < W) ? kc[w + 1] : kcR2;
+            if (!(mx[w] < EM1_TAU)) dM[w] = (kn1 - kn[w]) - (kc1 - kc[w]);
+          }
+        }
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          cb[r][lane][w] = colv[w] ? dM[w] : 0.0f;
+          cb[r][lane][W + w] = kc[w];
+          kc[w] = kn[w];
+          Eq[w] = Eqn[w];
+        }
+      }
+    };
+    for (int i0 = ((nrows - 1) / RC) * RC; i0 >= 0; i0 -= RC) {
+      const int nr = nrows - i0 < RC ? nrows - i0 : RC;
+      chunk_fwd(i0, nr);
+      for (int r = nr - 1; r >= 0; --r) {
+        float dM[W], k0[W];
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          dM[w] = cb[r][lane][w];
+          k0[w] = cb[r][lane][W + w];
+        }
+        rev_row(i0 + r, dM, k0);
+      }
+    }
+  } else {
+    for (int i = nrows - 1; i >= 0; --i) {
+      float k0[W], dM[W];
+#pragma unroll
+      for (int w = 0; w < W; ++w) k0[w] = 1.0f;
+      cells(fxc + (long long)i * FS, k0, kr1, 0.0f, 0.0f, dM);
+      rev_row(i, dM, k0);
+    }
   }
   {
     float Kh[W];
