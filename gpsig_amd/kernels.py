@@ -27,6 +27,14 @@ from . import ops
 DEFAULT_JITTER = 1e-6  # GPflow 1.5.1 settings.jitter (third-party default, unpinned in this image)
 
 
+def _params_to(obj, device, names):
+    """Move the named hyperparameter tensors of a kernel object to `device` (leaves stay leaves)."""
+    for n in names:
+        t = getattr(obj, n, None)
+        if isinstance(t, torch.Tensor):
+            setattr(obj, n, t.detach().to(device).requires_grad_(t.requires_grad))
+
+
 def _as_tensor(X, device=None):
     if isinstance(X, torch.Tensor):
         return X if device is None else X.to(device)
@@ -249,6 +257,13 @@ class SignatureKernel:
         return K if return_levels else K.sum(0)
 
     # ------------------------------------------------------------------ public API
+    def to(self, device):
+        """Keep variances, lengthscales, lags and gamma on `device` (sigma stays a host scalar), so a
+        call makes no host-to-device copies -- required for hipGraph capture (gpsig_amd.graphs).
+        Returns self."""
+        _params_to(self, device, ("variances", "lengthscales", "lags", "gamma"))
+        return self
+
     def K(self, X, X2=None, presliced=False, return_levels=False, presliced_X=False, presliced_X2=False):
         """kernels.py:402-477: (N, N2) or (num_levels+1, N, N2) with return_levels."""
         if presliced:

@@ -91,6 +91,12 @@ class UntruncSignatureKernel:
             X = X * self.gamma.to(X.device, X.dtype)[None, None, :, None]
         return X.reshape(N, Ln, num_features)
 
+    def to(self, device):
+        """Keep lengthscales, lags and gamma on `device` (see SignatureKernel.to).  Returns self."""
+        from .kernels import _params_to
+        _params_to(self, device, ("lengthscales", "lags", "gamma"))
+        return self
+
     def _prep(self, X):
         X = _as_tensor(X)
         N = X.shape[0]

@@ -84,3 +84,17 @@ def test_vjp_and_feature_entry_points_validate_arguments():
     assert lib.gpsig_signature_vjp(None, 4, 10, 3, 3, None, None, None) == L.GPSIG_EINVAL
     assert lib.gpsig_signature_channels(5, 3) == 5 + 25 + 125
     assert lib.gpsig_pde_vjp_workspace_bytes(2, 10, 10, 1) == 2 * 19 * 19 * 8
+
+
+def test_graph_capture_refuses_host_tensors_and_kernel_to():
+    """gpsig_amd.graphs.GraphedCall takes device tensors only; kern.to() keeps parameter leaves."""
+    import torch
+    import gpsig_amd
+    from gpsig_amd.graphs import GraphedCall
+    with pytest.raises(ValueError):
+        GraphedCall(lambda a: a, torch.zeros(2))
+    k = gpsig_amd.SignatureRBF(20, 2, 3, lengthscales=[1.0, 2.0])
+    k.lengthscales.requires_grad_(True)
+    k.to("cpu")
+    assert k.lengthscales.is_leaf and k.lengthscales.requires_grad
+    assert gpsig_amd.UntruncSignatureKernel(20, 2).to("cpu").num_features == 2
