@@ -19,8 +19,9 @@
 namespace gpsig {
 
 // DIAGK: the diagonal pass (pairs (a, a)) is the same body under its own symbol, so profiler
-// statistics of the Gram launch are not mixed with it.
-template <int DP, int W, int LP, int M, int SEED, bool DIAGK>
+// statistics of the Gram launch are not mixed with it.  SAVE: also write the VJP's saved state
+// (gpsig_sig_gram_state) -- a separate instantiation, so the plain Gram keeps its register budget.
+template <int DP, int W, int LP, int M, int SEED, bool DIAGK, bool SAVE = false>
 #ifdef GPSIG_FO_LB
 #define GPSIG_FO_BOUNDS __launch_bounds__(256, GPSIG_FO_LB)
 #else
@@ -148,6 +149,25 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
     do_row(rd, anch);
   }
 
+  // ---- saved VJP state (gpsig_sig_gram_state): column sums of levels 1..M-1 (column pair k holds
+  // columns k, k + W/2), before the epilogue so it adds no live registers there
+  static_assert(!SAVE || (!DIAGK && Seed::DIFF), "saved state: Gram pairs of a DIFF seed");
+  if constexpr (SAVE) {
+    if (pair_ok) {
+      const int nc = p.l2 - 1;
+      float *__restrict__ st = p.state + state_slot(a, b, p.n2, p.pair_mode == GPSIG_PAIRS_UPPER) * state_stride(M, p.l2);
+#pragma unroll
+      for (int m = 0; m + 1 < M; ++m)
+#pragma unroll
+        for (int w2 = 0; w2 < W2; ++w2)
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const int j = gl * W + w2 + h * W2;
+            if (j < nc) st[(long long)m * nc + j] = C[m][w2][h];
+          }
+    }
+  }
+
   // ---- epilogue: K_m = sum_j C_m(j)
   float K[M + 1];
   K[0] = 1.0f;
@@ -161,23 +181,11 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
   if (gl == 0 && pair_ok) {
     if constexpr (Seed::DIFF) K[1] = level1_closed<DP, SEED>(fx, fy, p.l1, p.l2);
     store_pair<M>(p, a, b, K);
-  }
-  if constexpr (!DIAGK && Seed::DIFF) {
-    if (p.state && pair_ok) {  // end-of-sweep state for the VJP (column pair k = columns k, k + W/2)
-      const int nc = p.l2 - 1;
-      float *__restrict__ st = p.state + state_slot(a, b, p.n2, p.pair_mode == GPSIG_PAIRS_UPPER) * state_stride(M, p.l2);
+    if constexpr (SAVE) {  // raw levels K_1..K_M after the column sums
+      float *__restrict__ st = p.state + state_slot(a, b, p.n2, p.pair_mode == GPSIG_PAIRS_UPPER) * state_stride(M, p.l2) +
+                               (long long)(M - 1) * (p.l2 - 1);
 #pragma unroll
-      for (int m = 0; m + 1 < M; ++m)
-#pragma unroll
-        for (int w2 = 0; w2 < W2; ++w2)
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int j = gl * W + w2 + h * W2;
-            if (j < nc) st[(long long)m * nc + j] = C[m][w2][h];
-          }
-      if (gl == 0)
-#pragma unroll
-        for (int m = 1; m <= M; ++m) st[(long long)(M - 1) * nc + m - 1] = K[m];
+      for (int m = 1; m <= M; ++m) st[m - 1] = K[m];
     }
   }
 }
@@ -209,10 +217,17 @@ constexpr int FO_MAX_LEVELS = 8;
 template <int DP, int W, int LP, int M, int SEED>
 int launch_fo(const SigArgs &a, long long nblocks, hipStream_t s) {
   if (nblocks <= 0) return GPSIG_OK;
-  if (a.pair_mode == GPSIG_PAIRS_DIAG)
+  constexpr bool DIFF = SEED == SEED_RBF_DIFF || SEED == SEED_LIN_DIFF;
+  if (a.pair_mode == GPSIG_PAIRS_DIAG) {
     hipLaunchKernelGGL((sig_fo_kernel<DP, W, LP, M, SEED, true>), dim3((unsigned)nblocks), dim3(256), 0, s, a);
-  else
+  } else if (a.state) {
+    if constexpr (DIFF)
+      hipLaunchKernelGGL((sig_fo_kernel<DP, W, LP, M, SEED, false, true>), dim3((unsigned)nblocks), dim3(256), 0, s, a);
+    else
+      return GPSIG_EUNSUPPORTED;
+  } else {
     hipLaunchKernelGGL((sig_fo_kernel<DP, W, LP, M, SEED, false>), dim3((unsigned)nblocks), dim3(256), 0, s, a);
+  }
   return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
 }
 

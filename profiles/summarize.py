@@ -6,7 +6,8 @@
 writes profiles/<tag>_kernel_stats.csv (rocprofv3 --stats summary, as produced),
 profiles/<tag>_gram_counters.json (per-launch counters of the Gram kernel, HBM bytes with the gfx950
 FETCH_SIZE correction of MI355X_MICROARCH.md 'HBM': bytes = (2 * FETCH_SIZE + WRITE_SIZE) * 1024).
-The Gram kernel is sig_fo_kernel with DIAGK = false (the diagonal pass has its own symbol).
+The Gram kernel is sig_fo_kernel with DIAGK = SAVE = false (the diagonal pass and the training
+variant that saves the VJP state have their own symbols).
 """
 import csv
 import glob
@@ -21,7 +22,8 @@ here = os.path.dirname(os.path.abspath(__file__))
 
 
 def is_gram(name):
-    return "sig_fo_kernel" in name and ("false>" in name or "Lb0E" in name)
+    # sig_fo_kernel<DP, W, LP, M, SEED, DIAGK = false, SAVE = false>
+    return "sig_fo_kernel" in name and ("false, false>" in name or "Lb0ELb0E" in name)
 
 
 def one(pattern):
