@@ -46,7 +46,7 @@ SIGNATURES = {
     "gpsig_sig_gram": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I,
                             _P, _P, _P, _F, _I, _P, _I, _I, _P, _SZ, _P]),
     "gpsig_sig_diag": (_I, [_P, _I, _I, _I, _I, _I, _I, _I, _F, _I, _P, _P, _SZ, _P]),
-    "gpsig_sig_gram_vjp": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _I,
+    "gpsig_sig_gram_vjp": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _I,
                                 _P, _P, _P, _F, _P, _P, _P, _P, _P, _P, _P, _SZ, _P]),
     "gpsig_sig_state_bytes": (_SZ, [_I, _I, _I, _I, _I]),
     "gpsig_sig_gram_state": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _F, _I, _P,

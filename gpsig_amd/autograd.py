@@ -14,8 +14,9 @@ When a gradient is needed, the forward Gram launch also saves its end-of-sweep s
 sweep; above GRAM_STATE_BYTES (env GPSIG_GRAM_STATE_BYTES) the VJP recomputes it instead.
 
 Gradients reach the sequences (and, through the host-side scaling in kernels.py, the lengthscales)
-and sigma * variances.  Supported for order == 1 with difference == True (the reference defaults);
-other configurations evaluate forward but raise NotImplementedError on backward.
+and sigma * variances.  Supported for order == 1 (difference True or False for K / Kdiag; True for the
+inducing-tensor kernels); other configurations evaluate forward but raise NotImplementedError on
+backward.
 """
 from __future__ import annotations
 
@@ -30,10 +31,12 @@ from . import ops
 GRAM_STATE_BYTES = int(os.environ.get("GPSIG_GRAM_STATE_BYTES", 16 << 30))
 
 
-def _check_bwd(cfg):
-    if cfg["order"] != 1 or not cfg["difference"]:
-        raise NotImplementedError("gradients of the signature kernels are implemented for order=1 and "
-                                  "difference=True (gpsig_sig_gram_vjp, gpsig_tens_vs_seq_vjp)")
+def _check_bwd(cfg, gram=False):
+    """Gram / diagonal VJP: order 1, difference True or False; inducing-tensor VJPs: order 1,
+    difference True."""
+    if cfg["order"] != 1 or not (gram or cfg["difference"]):
+        raise NotImplementedError("gradients of the signature kernels are implemented for order=1 (Gram, "
+                                  "gpsig_sig_gram_vjp) and order=1, difference=True (gpsig_tens_vs_seq_vjp)")
 
 
 class SigGram(torch.autograd.Function):
@@ -67,7 +70,7 @@ class SigGram(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gout):
         cfg = ctx.cfg
-        _check_bwd(cfg)
+        _check_bwd(cfg, gram=True)
         Xs, X2s, sc32, rs1, rs2 = ctx.saved_tensors
         M = cfg["num_levels"]
         sym = X2s is None
@@ -81,14 +84,17 @@ class SigGram(torch.autograd.Function):
         gscale = torch.zeros((M + 1,), dtype=torch.float32, device=dev)
         jit = cfg["jitter"] if (cfg["normalization"] and sym) else 0.0
         gX, gY = ops.sig_gram_vjp(Xs.detach(), None if sym else X2s.detach(), M, gout, base=cfg["base"],
+                                  difference=cfg["difference"],
                                   gout_levels=cfg["return_levels"], rs1=rs1, rs2=rs2, scale=sc32, jitter=jit,
                                   grs1=grs1, grs2=grs2, gscale=gscale, state=ctx.state)
         ctx.state = None
         if cfg["normalization"]:
             # rs = (K_m(a, a) + jitter)^-1/2  ->  dLoss/dK_m(a, a) = -rs^3/2 dLoss/drs
-            ops.sig_gram_vjp(Xs.detach(), None, M, grs1 * (-0.5) * rs1 ** 3, base=cfg["base"], diag=True, gX=gX)
+            ops.sig_gram_vjp(Xs.detach(), None, M, grs1 * (-0.5) * rs1 ** 3, base=cfg["base"], diag=True, gX=gX,
+                             difference=cfg["difference"])
             if not sym:
                 ops.sig_gram_vjp(X2s.detach(), None, M, grs2 * (-0.5) * rs2 ** 3, base=cfg["base"], diag=True,
+                                 difference=cfg["difference"],
                                  gX=gY)
         gXo = gX.to(Xs.dtype) if ctx.needs_input_grad[0] else None
         gYo = gY.to(X2s.dtype) if (not sym and ctx.needs_input_grad[1]) else None
@@ -108,9 +114,10 @@ class SigDiag(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gout):
         cfg = ctx.cfg
-        _check_bwd(cfg)
+        _check_bwd(cfg, gram=True)
         (Xs,) = ctx.saved_tensors
-        gX, _ = ops.sig_gram_vjp(Xs.detach(), None, cfg["num_levels"], gout, base=cfg["base"], diag=True)
+        gX, _ = ops.sig_gram_vjp(Xs.detach(), None, cfg["num_levels"], gout, base=cfg["base"], diag=True,
+                                 difference=cfg["difference"])
         return gX.to(Xs.dtype), None
 
 

@@ -107,11 +107,12 @@ template <int DP, int W, int LP, int M, int SEED>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_WPE))) void sig_bwd_kernel(BwdArgs p) {
   constexpr int FS = feat_stride(DP);
   constexpr int G = 64 / LP;
-  constexpr bool RBF = (SEED == SEED_RBF_DIFF);
+  constexpr bool DIFF = (SEED == SEED_RBF_DIFF || SEED == SEED_LIN_DIFF);  // else difference=False
+  constexpr bool RBF = (SEED == SEED_RBF_DIFF || SEED == SEED_RBF_POINT);   // base kernel
   constexpr float NHL2E = -0.72134752044448170f;  // exp(-d2/2) = exp2(d2 * NHL2E)
   constexpr float L2E = 1.4426950408889634f;
   constexpr int RC = W >= 4 ? 4 : 8;  // rows per chunk of the reverse sweep (<= the forward's anchor period)
-  __shared__ __attribute__((aligned(16))) float cbuf[RBF ? 4 : 1][RBF ? RC : 1][64][2 * W];
+  __shared__ __attribute__((aligned(16))) float cbuf[RBF && DIFF ? 4 : 1][RBF && DIFF ? RC : 1][64][2 * W];
   constexpr int ML = M > 1 ? M - 1 : 1;
 
   const int lane = threadIdx.x & 63;
@@ -156,7 +157,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
 #pragma unroll
   for (int w = 0; w < W; ++w) {
     const int j = gl * W + w;
-    colv[w] = j < l2 - 1;
+    colv[w] = j < (DIFF ? l2 - 1 : l2);  // columns of the grid the recursion consumes
     ptv[w] = j < l2;
     const int jj = j < l2 ? j : l2 - 1;
     const float *f = fy + (long long)jj * FS;
@@ -226,8 +227,29 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
   float kc[W], kcR = 0.0f;
   float K[M + 1];
   K[0] = 1.0f;
-  const int nrows = l1 - 1;
-  const bool saved = p.state != nullptr;  // kernel-uniform
+  const int nrows = DIFF ? l1 - 1 : l1;
+  const bool saved = DIFF && p.state != nullptr;  // kernel-uniform (the host passes state for DIFF only)
+  // difference=False: the cells are the point grid itself, k(x_i, y_j) (signature_algs.py:26 skipped)
+  auto point_cells = [&](int i, float (&dM)[W], float (&k0)[W]) {
+    cfloat *xr = fxc + (long long)i * FS;
+    if constexpr (RBF) {
+      krow(xr, k0);
+#pragma unroll
+      for (int w = 0; w < W; ++w) dM[w] = colv[w] ? k0[w] : 0.0f;
+    } else {
+      float xv[DP];
+#pragma unroll
+      for (int k = 0; k < DP; ++k) xv[k] = xr[k];
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        float c = 0.0f;
+#pragma unroll
+        for (int k = 0; k < DP; ++k) c = __builtin_fmaf(xv[k], y[w][k], c);
+        dM[w] = colv[w] ? c : 0.0f;
+        k0[w] = 1.0f;
+      }
+    }
+  };
   if (saved) {
     const int nc = l2 - 1;
     const float *__restrict__ st =
@@ -246,18 +268,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
       kcR = lane_next(kc[0]);
     }
   } else {
-    if constexpr (RBF) {
+    if constexpr (RBF && DIFF) {
       krow(fxc, kc);
       kcR = lane_next(kc[0]);
     }
     for (int i = 0; i < nrows; ++i) {
       cfloat *fr = fxc + (long long)i * FS;
       float kn[W], knR = 0.0f, dM[W];
-      if constexpr (RBF) {
-        krow(fr + FS, kn);
-        knR = lane_next(kn[0]);
+      if constexpr (DIFF) {
+        if constexpr (RBF) {
+          krow(fr + FS, kn);
+          knR = lane_next(kn[0]);
+        }
+        cells(fr, kc, kn, kcR, knR, dM);
+      } else {
+        point_cells(i, dM, kn);
       }
-      cells(fr, kc, kn, kcR, knR, dM);
       if constexpr (M > 1) {
         float Cs[ML][W], S[ML][W];
 #pragma unroll
@@ -272,7 +298,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
       }
 #pragma unroll
       for (int w = 0; w < W; ++w) C[0][w] += dM[w];
-      if constexpr (RBF) {
+      if constexpr (RBF && DIFF) {
 #pragma unroll
         for (int w = 0; w < W; ++w) kc[w] = kn[w];
         kcR = knR;
@@ -286,7 +312,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
       for (int w = 0; w < W; ++w) s += C[m][w];
       K[m + 1] = group_sum<LP>(s);
     }
-    K[1] = level1_closed<DP, SEED>(fx, fy, l1, l2);
+    if constexpr (DIFF) K[1] = level1_closed<DP, SEED>(fx, fy, l1, l2);
   }
 
   // ---- per-level weights g_m = dLoss/dK_m(a, b) and the normalisation / scale terms
@@ -387,8 +413,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
     }
   };
 
-  float kr1[W];  // k row of point i+1
-  if constexpr (RBF) {
+  float kr1[W];  // k row of point i+1 (DIFF)
+  if constexpr (RBF && DIFF) {
 #pragma unroll
     for (int w = 0; w < W; ++w) kr1[w] = kc[w];
   } else {
@@ -435,22 +461,26 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
         for (int w = 0; w < W; ++w) Ch[m][w] += r[m][w];
     }
 
-    // adjoint of the second difference: E(i, j) = Dh(i, j-1) - Dh(i, j); Kh(i+1, j) = E(i, j) - E(i+1, j)
-    float left = lane_prev(Dh[W - 1]);
-    if (gl == 0) left = 0.0f;
-    float Kh[W];
+    if constexpr (DIFF) {
+      // adjoint of the second difference: E(i, j) = Dh(i, j-1) - Dh(i, j); Kh(i+1, j) = E(i, j) - E(i+1, j)
+      float left = lane_prev(Dh[W - 1]);
+      if (gl == 0) left = 0.0f;
+      float Kh[W];
 #pragma unroll
-    for (int w = 0; w < W; ++w) {
-      const float e = ((w == 0) ? left : Dh[w - 1]) - Dh[w];
-      Kh[w] = e - Ep[w];
-      Ep[w] = e;
+      for (int w = 0; w < W; ++w) {
+        const float e = ((w == 0) ? left : Dh[w - 1]) - Dh[w];
+        Kh[w] = e - Ep[w];
+        Ep[w] = e;
+      }
+      emit(i + 1, Kh, kr1);
+#pragma unroll
+      for (int w = 0; w < W; ++w) kr1[w] = k0[w];
+    } else {
+      emit(i, Dh, k0);  // the cell is the point value: dLoss/dk(x_i, y_j) = Dh(i, j)
     }
-    emit(i + 1, Kh, kr1);
-#pragma unroll
-    for (int w = 0; w < W; ++w) kr1[w] = k0[w];
   };
 
-  if constexpr (RBF) {
+  if constexpr (RBF && DIFF) {
     // Chunked: the cells of RC rows are regenerated forward from an exact row (k and expm1(q) from
     // x - y) with the exp-free recurrences of the forward kernel (sig_common.h RbfSeedPk; chunk
     // starts at multiples of RC <= its anchor period, so the cells are the forward launch's) into
@@ -534,7 +564,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
         rev_row(i0 + r, dM, k0);
       }
     }
-  } else {
+  } else if constexpr (DIFF) {
     for (int i = nrows - 1; i >= 0; --i) {
       float k0[W], dM[W];
 #pragma unroll
@@ -542,8 +572,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
       cells(fxc + (long long)i * FS, k0, kr1, 0.0f, 0.0f, dM);
       rev_row(i, dM, k0);
     }
+  } else {
+    for (int i = nrows - 1; i >= 0; --i) {
+      float k0[W], dM[W];
+      point_cells(i, dM, k0);
+      rev_row(i, dM, k0);
+    }
   }
-  {
+  if constexpr (DIFF) {
     float Kh[W];
 #pragma unroll
     for (int w = 0; w < W; ++w) Kh[w] = -Ep[w];

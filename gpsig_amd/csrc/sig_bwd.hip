@@ -39,22 +39,23 @@ static inline long long upper_prefix(long long r, long long ntb, long long k) { 
 using namespace gpsig;
 
 extern "C" int gpsig_sig_gram_vjp(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d,
-                                  int num_levels, int base_kind, int pair_mode, int row_begin, int row_end,
+                                  int num_levels, int base_kind, int difference, int pair_mode, int row_begin, int row_end,
                                   const float *gout, int gout_levels, const float *rs1, const float *rs2,
                                   const float *scale, float jitter, float *gX, float *gY, float *grs1, float *grs2,
                                   float *gscale, const float *state, void *workspace, size_t workspace_bytes,
                                   gpsig_stream_t stream) {
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (!X || !Y || !gout || !gX || n1 <= 0 || n2 <= 0 || d <= 0 || num_levels < 1) return GPSIG_EINVAL;
-  if (l1 < 2 || l2 < 2) return GPSIG_EINVAL;
+  if (l1 < 1 || l2 < 1 || (difference && (l1 < 2 || l2 < 2))) return GPSIG_EINVAL;
   if (pair_mode < GPSIG_PAIRS_RECT || pair_mode > GPSIG_PAIRS_DIAG) return GPSIG_EINVAL;
   if (row_begin < 0 || row_end > n1 || row_begin > row_end) return GPSIG_EINVAL;
   if (pair_mode != GPSIG_PAIRS_RECT && (n1 != n2 || l1 != l2 || X != Y)) return GPSIG_EINVAL;
   if (pair_mode == GPSIG_PAIRS_RECT && !gY) return GPSIG_EINVAL;
   if (pair_mode == GPSIG_PAIRS_DIAG && !gout_levels) return GPSIG_EINVAL;
   if ((rs1 == nullptr) != (rs2 == nullptr)) return GPSIG_EINVAL;
-  if (state && pair_mode == GPSIG_PAIRS_DIAG) return GPSIG_EINVAL;
-  const int seed = base_kind == GPSIG_BASE_RBF ? SEED_RBF_DIFF : (base_kind == GPSIG_BASE_LINEAR ? SEED_LIN_DIFF : -1);
+  if (state && (pair_mode == GPSIG_PAIRS_DIAG || !difference)) return GPSIG_EINVAL;
+  const int seed = base_kind == GPSIG_BASE_RBF ? (difference ? SEED_RBF_DIFF : SEED_RBF_POINT)
+                   : base_kind == GPSIG_BASE_LINEAR ? (difference ? SEED_LIN_DIFF : SEED_LIN_POINT) : -1;
   const int DP = bwd_pad(d);
   if (seed < 0 || DP == 0) return GPSIG_EUNSUPPORTED;
   const BwdGeo geo = bwd_geometry(l2, DP);

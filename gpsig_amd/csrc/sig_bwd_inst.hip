@@ -28,6 +28,8 @@ int sig_bwd_launch_dpm(const BwdArgs &a, int seed, long long nblocks, hipStream_
   switch (seed) {
     case SEED_RBF_DIFF: return bwd_geo<DP, M, SEED_RBF_DIFF>(a, nblocks, s);
     case SEED_LIN_DIFF: return bwd_geo<DP, M, SEED_LIN_DIFF>(a, nblocks, s);
+    case SEED_RBF_POINT: return bwd_geo<DP, M, SEED_RBF_POINT>(a, nblocks, s);
+    case SEED_LIN_POINT: return bwd_geo<DP, M, SEED_LIN_POINT>(a, nblocks, s);
     default: return GPSIG_EUNSUPPORTED;
   }
 }

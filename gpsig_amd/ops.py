@@ -140,7 +140,8 @@ def sig_state_numel(n1: int, n2: int | None, l2: int, num_levels: int) -> int:
 def sig_gram_vjp(X: torch.Tensor, Y: torch.Tensor | None, num_levels: int, gout: torch.Tensor, base="rbf",
                  gout_levels: bool = False, diag: bool = False, rs1=None, rs2=None, scale=None, jitter: float = 0.0,
                  gX: torch.Tensor | None = None, gY: torch.Tensor | None = None, grs1=None, grs2=None,
-                 gscale=None, rows: tuple | None = None, state: torch.Tensor | None = None):
+                 gscale=None, rows: tuple | None = None, state: torch.Tensor | None = None,
+                 difference: bool = True):
     """dLoss/dX (and dLoss/dY, dLoss/drs, dLoss/dscale) of the first-order Gram, accumulated into float32
     buffers: see gpsig_sig_gram_vjp in include/gpsig_amd.h.  Y None -> symmetric K(X) (or the diagonal
     with diag=True; gout is then (num_levels+1, n) per level).  state: the buffer a sig_gram(...,
@@ -182,7 +183,8 @@ def sig_gram_vjp(X: torch.Tensor, Y: torch.Tensor | None, num_levels: int, gout:
     nb = lib.gpsig_sig_workspace_bytes(n1, l1, n2, l2, d)
     ws = workspace(X.device, nb)
     mode = L.PAIRS_DIAG if diag else (L.PAIRS_UPPER if sym else L.PAIRS_RECT)
-    rc = lib.gpsig_sig_gram_vjp(X.data_ptr(), n1, l1, Y.data_ptr(), n2, l2, d, num_levels, base_kind(base), mode, r0, r1,
+    rc = lib.gpsig_sig_gram_vjp(X.data_ptr(), n1, l1, Y.data_ptr(), n2, l2, d, num_levels, base_kind(base),
+                                int(bool(difference)), mode, r0, r1,
                                 gout.data_ptr(), int(bool(gout_levels)), _ptr(rs1), _ptr(rs2), _ptr(scale),
                                 float(jitter), gX.data_ptr(), _ptr(gY), _ptr(grs1), _ptr(grs2), _ptr(gscale),
                                 _ptr(state), ws.data_ptr(), ws.numel(), _stream(X.device))

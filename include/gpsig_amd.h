@@ -108,7 +108,8 @@ int gpsig_sig_diag(const float *X, int n, int l, int d, int num_levels, int orde
  * The reference obtains dLoss/dX of K (and through the host-side scaling dLoss/dlengthscales) by TF
  * autodiff of the graph kernels.py:209-238 (base kernel, kernels.py:946-1044) ->
  * signature_algs.py:8-35 -> kernels.py:431-477 (jitter, normalisation, sigma*variances).  This entry
- * evaluates the same derivative for order == 1 and difference == True (RBF and linear seeds):
+ * evaluates the same derivative for order == 1, RBF and linear base kernels, difference == 1 (second
+ * difference of the base-kernel grid, the default) or 0 (the grid itself, kernels.py:19 `difference`):
  *
  *   gout_levels == 0: gout (n1, n2) is dLoss/dK for out_mode GPSIG_OUT_NORM_SUM;
  *   gout_levels == 1: gout (L+1, n1, n2) is dLoss/dK_m for GPSIG_OUT_LEVELS / GPSIG_OUT_NORM_LEVELS;
@@ -121,7 +122,7 @@ int gpsig_sig_diag(const float *X, int n, int l, int d, int num_levels, int orde
  *   Workspace: gpsig_sig_workspace_bytes(n1, l1, n2, l2, d).
  */
 int gpsig_sig_gram_vjp(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int num_levels,
-                       int base_kind, int pair_mode, int row_begin, int row_end, const float *gout, int gout_levels,
+                       int base_kind, int difference, int pair_mode, int row_begin, int row_end, const float *gout, int gout_levels,
                        const float *rs1, const float *rs2, const float *scale, float jitter, float *gX, float *gY,
                        float *grs1, float *grs2, float *gscale, const float *state, void *workspace,
                        size_t workspace_bytes, gpsig_stream_t stream);

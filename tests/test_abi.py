@@ -67,7 +67,7 @@ def test_vjp_and_feature_entry_points_validate_arguments():
     """The gradient / signature entry points reject null pointers and bad shapes before any HIP call."""
     import gpsig_amd._lib as L
     lib = L.load()
-    assert lib.gpsig_sig_gram_vjp(None, 4, 10, None, 4, 10, 3, 4, 0, 0, 0, 4, None, 0, None, None, None, 0.0,
+    assert lib.gpsig_sig_gram_vjp(None, 4, 10, None, 4, 10, 3, 4, 0, 1, 0, 0, 4, None, 0, None, None, None, 0.0,
                                   None, None, None, None, None, None, None, 0, None) == L.GPSIG_EINVAL
     assert lib.gpsig_sig_gram_state(None, 4, 10, None, 4, 10, 3, 4, 0, 0, 0, 4, None, None, None, 0.0, 0, None,
                                     0, 4, None, 0, None, 0, None) == L.GPSIG_EINVAL

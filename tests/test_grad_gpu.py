@@ -124,6 +124,45 @@ def test_rough_data_vjp():
     assert norm_rel_err(got[0], ref[0]) < GTOL
 
 
+@pytest.mark.parametrize("base", ["rbf", "linear"])
+@pytest.mark.parametrize("cross", [False, True])
+def test_gram_vjp_no_difference(base, cross):
+    """difference=False (the base-kernel grid itself feeds the recursion): normalised K gradients
+    w.r.t. the sequences and the variances vs fp64 autodiff."""
+    import gpsig_amd
+    N, N2, L, D, M = 10, 7, 21, 3, 4
+    X = walks(N, L, D, 40)
+    X2 = walks(N2, L, D, 41) if cross else None
+    G = np.random.default_rng(42).standard_normal((N, N2 if cross else N))
+    cls = gpsig_amd.SignatureRBF if base == "rbf" else gpsig_amd.SignatureLinear
+    k = cls(L * D, D, M, difference=False)
+    k.variances.requires_grad_(True)
+    got, _ = grads_gpu(k, X, X2, G, params=(k.variances,))
+    Xt = torch.tensor(X, requires_grad=True)
+    X2t = None if X2 is None else torch.tensor(X2, requires_grad=True)
+    var = torch.ones(M + 1, dtype=torch.float64, requires_grad=True)
+    K = ar.K(Xt, X2t, M, base=base, scale=var, difference=False)
+    (K * torch.tensor(G)).sum().backward()
+    assert norm_rel_err(got[0], Xt.grad.numpy()) < GTOL
+    if cross:
+        assert norm_rel_err(got[1], X2t.grad.numpy()) < GTOL
+    assert norm_rel_err(got[-1], var.grad.numpy()) < GTOL
+
+
+@pytest.mark.parametrize("base", ["rbf", "linear"])
+def test_raw_levels_vjp_no_difference_ragged(base):
+    from gpsig_amd import ops
+    N1, N2, L1, L2, D, M = 4, 6, 13, 40, 5, 5
+    X, Y = walks(N1, L1, D, 43), walks(N2, L2, D, 44)
+    G = np.random.default_rng(45).standard_normal((M + 1, N1, N2))
+    gX, gY = ops.sig_gram_vjp(torch.tensor(X, device=DEV), torch.tensor(Y, device=DEV), M,
+                              torch.tensor(G, device=DEV), base=base, gout_levels=True, difference=False)
+    Xr, Yr = torch.tensor(X, requires_grad=True), torch.tensor(Y, requires_grad=True)
+    (ar.k_seq(Xr, Yr, M, base, difference=False) * torch.tensor(G)).sum().backward()
+    assert norm_rel_err(gX.cpu().numpy(), Xr.grad.numpy()) < GTOL
+    assert norm_rel_err(gY.cpu().numpy(), Yr.grad.numpy()) < GTOL
+
+
 def test_higher_order_backward_raises():
     import gpsig_amd
     X = walks(4, 10, 2, 0)
