@@ -14,9 +14,8 @@ When a gradient is needed, the forward Gram launch also saves its end-of-sweep s
 sweep; above GRAM_STATE_BYTES (env GPSIG_GRAM_STATE_BYTES) the VJP recomputes it instead.
 
 Gradients reach the sequences (and, through the host-side scaling in kernels.py, the lengthscales)
-and sigma * variances.  Supported for order == 1 (difference True or False for K / Kdiag; True for the
-inducing-tensor kernels); other configurations evaluate forward but raise NotImplementedError on
-backward.
+and sigma * variances.  Supported for order == 1 (difference True or False); higher orders evaluate
+forward but raise NotImplementedError on backward.
 """
 from __future__ import annotations
 
@@ -32,11 +31,10 @@ GRAM_STATE_BYTES = int(os.environ.get("GPSIG_GRAM_STATE_BYTES", 16 << 30))
 
 
 def _check_bwd(cfg, gram=False):
-    """Gram / diagonal VJP: order 1, difference True or False; inducing-tensor VJPs: order 1,
-    difference True."""
-    if cfg["order"] != 1 or not (gram or cfg["difference"]):
-        raise NotImplementedError("gradients of the signature kernels are implemented for order=1 (Gram, "
-                                  "gpsig_sig_gram_vjp) and order=1, difference=True (gpsig_tens_vs_seq_vjp)")
+    """The VJP kernels cover order 1 (difference True or False)."""
+    if cfg["order"] != 1:
+        raise NotImplementedError("gradients of the signature kernels are implemented for order=1 "
+                                  "(gpsig_sig_gram_vjp, gpsig_tens_vs_seq_vjp)")
 
 
 class SigGram(torch.autograd.Function):
@@ -135,10 +133,10 @@ class TensVsSeq(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gout):
         cfg = ctx.cfg
-        _check_bwd(cfg)
+        _check_bwd(cfg, gram=True)
         Zs, Xs = ctx.saved_tensors
         gZ, gX = ops.tens_vs_seq_vjp(Zs.detach(), Xs.detach(), cfg["num_levels"], gout, cfg["base"],
-                                     cfg["increments"])
+                                     cfg["increments"], difference=cfg["difference"])
         return (gZ.to(Zs.dtype) if ctx.needs_input_grad[0] else None,
                 gX.to(Xs.dtype) if ctx.needs_input_grad[1] else None, None)
 

@@ -32,7 +32,8 @@ struct TvsBwdArgs {
 
 // Level I only (levels are independent chains; blockIdx.z selects the level, so the per-lane state is
 // O(I * DP) and not O(M^2 * DP)).  LT below is the number of components of this level.
-template <int DP, int I, bool INCR, bool RBF>
+// DIFF = false (difference=False): the cells are the point values P_k(s) themselves, s = 0..L-1.
+template <int DP, int I, bool INCR, bool RBF, bool DIFF>
 __device__ __forceinline__ void tvs_bwd_level(const TvsBwdArgs &a) {
   constexpr int LT = I;
   constexpr int KB = I * (I - 1) / 2;  // first component of the level
@@ -125,33 +126,65 @@ __device__ __forceinline__ void tvs_bwd_level(const TvsBwdArgs &a) {
   float A[LT], pv0[LT], pv1[LT];
 #pragma unroll
   for (int k = 0; k < LT; ++k) A[k] = 0.f;
-  {
-    float x0[DP];
-    ldx(0, x0);
+  // point value P_k at x (difference=False cell): RBF k(z0, x) [k(z1, x) - k(z0, x)], linear <z, x>
+  auto pcell = [&](int k, const float (&x)[DP], float v0, float v1) -> float {
+    if constexpr (RBF) {
+      return INCR ? v1 - v0 : v0;
+    } else {
+      float v = 0.f;
 #pragma unroll
-    for (int k = 0; k < LT; ++k) pvals(k, x0, pv0[k], pv1[k]);
-  }
-  for (int s = 0; s < L - 1; ++s) {
-    float x[DP], dx[DP], xn[DP];
-    ldx(s, x);
+      for (int q = 0; q < DP; ++q) v = __builtin_fmaf(INCR ? z1c(k, q) - z0c(k, q) : z0c(k, q), x[q], v);
+      return v;
+    }
+  };
+  if constexpr (DIFF) {
+    {
+      float x0[DP];
+      ldx(0, x0);
 #pragma unroll
-    for (int q = 0; q < DP; ++q) dx[q] = q < d ? ld(s, d + q) : 0.f;
-    ldx(s + 1, xn);
-    const float gs = ld(s, 2 * d + 1);
-    float prev = 0.f;
+      for (int k = 0; k < LT; ++k) pvals(k, x0, pv0[k], pv1[k]);
+    }
+    for (int s = 0; s < L - 1; ++s) {
+      float x[DP], dx[DP], xn[DP];
+      ldx(s, x);
 #pragma unroll
-    for (int k = 0; k < I; ++k) {
-      float n0, n1;
-      pvals(k, xn, n0, n1);
-      const float m = cell(k, x, dx, gs, pv0[k], pv1[k], n0, n1);
-      pv0[k] = n0;
-      pv1[k] = n1;
-      if (k == 0) {
-        prev = m;
-      } else {
-        const float as = A[k - 1];
-        A[k - 1] = as + prev;
-        prev = m * as;
+      for (int q = 0; q < DP; ++q) dx[q] = q < d ? ld(s, d + q) : 0.f;
+      ldx(s + 1, xn);
+      const float gs = ld(s, 2 * d + 1);
+      float prev = 0.f;
+#pragma unroll
+      for (int k = 0; k < I; ++k) {
+        float n0, n1;
+        pvals(k, xn, n0, n1);
+        const float m = cell(k, x, dx, gs, pv0[k], pv1[k], n0, n1);
+        pv0[k] = n0;
+        pv1[k] = n1;
+        if (k == 0) {
+          prev = m;
+        } else {
+          const float as = A[k - 1];
+          A[k - 1] = as + prev;
+          prev = m * as;
+        }
+      }
+    }
+  } else {
+    for (int s = 0; s < L; ++s) {
+      float x[DP];
+      ldx(s, x);
+      float prev = 0.f;
+#pragma unroll
+      for (int k = 0; k < I; ++k) {
+        float v0, v1;
+        pvals(k, x, v0, v1);
+        const float m = pcell(k, x, v0, v1);
+        if (k == 0) {
+          prev = m;
+        } else {
+          const float as = A[k - 1];
+          A[k - 1] = as + prev;
+          prev = m * as;
+        }
       }
     }
   }
@@ -214,13 +247,14 @@ __device__ __forceinline__ void tvs_bwd_level(const TvsBwdArgs &a) {
   };
 
   // row s of the reverse sweep is loaded one step ahead (before the previous step's atomics)
+  const int stop = DIFF ? L - 2 : L - 1;  // last row of the grid the recursion consumes
   float xs1[DP], x[DP], dx[DP], gs;  // xs1 = x at s + 1
   ldx(L - 1, xs1);
-  ldx(L - 2, x);
+  ldx(stop, x);
 #pragma unroll
-  for (int q = 0; q < DP; ++q) dx[q] = q < d ? ld(L - 2, d + q) : 0.f;
-  gs = ld(L - 2, 2 * d + 1);
-  for (int s = L - 2; s >= 0; --s) {
+  for (int q = 0; q < DP; ++q) dx[q] = q < d ? ld(stop, d + q) : 0.f;
+  gs = ld(stop, 2 * d + 1);
+  for (int s = stop; s >= 0; --s) {
     float xn[DP], dxn[DP], gsn = 0.f;  // row s - 1
     const int sn = s > 0 ? s - 1 : 0;
     ldx(sn, xn);
@@ -235,7 +269,7 @@ __device__ __forceinline__ void tvs_bwd_level(const TvsBwdArgs &a) {
       for (int st = 0; st < i; ++st) {
         const int k = k0 + st;
         pvals(k, x, c0[k], c1[k]);
-        m[st] = cell(k, x, dx, gs, c0[k], c1[k], pv0[k], pv1[k]);
+        m[st] = DIFF ? cell(k, x, dx, gs, c0[k], c1[k], pv0[k], pv1[k]) : pcell(k, x, c0[k], c1[k]);
       }
       // A_j(s) = A_j(s+1) - M_{c_j}(s) A_{j-1}(s), ascending j (A_0 = 1)
       Av[0] = 1.0f;
@@ -250,7 +284,7 @@ __device__ __forceinline__ void tvs_bwd_level(const TvsBwdArgs &a) {
         const float Q = (j < i) ? Acc[k0 + j - 1] : gI;
         const float mh = Q * Av[j - 1];
         const int k = k0 + j - 1;
-        Ph[k] = mh - Mh[k];  // dLoss/dP_k(s+1) = dM_k(s) - dM_k(s+1)
+        Ph[k] = DIFF ? mh - Mh[k] : mh;  // dLoss/dP_k(s+1) = dM_k(s) - dM_k(s+1) [P_k(s) = M_k(s)]
         Mh[k] = mh;
       }
       // Q_j(s-1) = Q_j(s) + M_{c_{j+1}}(s) Q_{j+1}(s), ascending j (old Q_{j+1})
@@ -260,7 +294,10 @@ __device__ __forceinline__ void tvs_bwd_level(const TvsBwdArgs &a) {
         Acc[k0 + j - 1] = __builtin_fmaf(m[j], Qn, Acc[k0 + j - 1]);
       }
     }
-    emit(s + 1, Ph, pv0, pv1, xs1);
+    if constexpr (DIFF)
+      emit(s + 1, Ph, pv0, pv1, xs1);
+    else
+      emit(s, Ph, c0, c1, x);
 #pragma unroll
     for (int k = 0; k < LT; ++k) {
       pv0[k] = c0[k];
@@ -274,7 +311,7 @@ __device__ __forceinline__ void tvs_bwd_level(const TvsBwdArgs &a) {
     }
     gs = gsn;
   }
-  {
+  if constexpr (DIFF) {
     float Ph[LT];
 #pragma unroll
     for (int k = 0; k < LT; ++k) Ph[k] = -Mh[k];
@@ -311,17 +348,17 @@ __device__ __forceinline__ void tvs_bwd_level(const TvsBwdArgs &a) {
   }
 }
 
-template <int DP, int M, bool INCR, bool RBF>
+template <int DP, int M, bool INCR, bool RBF, bool DIFF>
 __global__ __launch_bounds__(64) void tvs_bwd_kernel(TvsBwdArgs a) {
   switch (blockIdx.z) {
-    case 0: tvs_bwd_level<DP, 1, INCR, RBF>(a); break;
-    case 1: if constexpr (M >= 2) tvs_bwd_level<DP, 2, INCR, RBF>(a); break;
-    case 2: if constexpr (M >= 3) tvs_bwd_level<DP, 3, INCR, RBF>(a); break;
-    case 3: if constexpr (M >= 4) tvs_bwd_level<DP, 4, INCR, RBF>(a); break;
-    case 4: if constexpr (M >= 5) tvs_bwd_level<DP, 5, INCR, RBF>(a); break;
-    case 5: if constexpr (M >= 6) tvs_bwd_level<DP, 6, INCR, RBF>(a); break;
-    case 6: if constexpr (M >= 7) tvs_bwd_level<DP, 7, INCR, RBF>(a); break;
-    case 7: if constexpr (M >= 8) tvs_bwd_level<DP, 8, INCR, RBF>(a); break;
+    case 0: tvs_bwd_level<DP, 1, INCR, RBF, DIFF>(a); break;
+    case 1: if constexpr (M >= 2) tvs_bwd_level<DP, 2, INCR, RBF, DIFF>(a); break;
+    case 2: if constexpr (M >= 3) tvs_bwd_level<DP, 3, INCR, RBF, DIFF>(a); break;
+    case 3: if constexpr (M >= 4) tvs_bwd_level<DP, 4, INCR, RBF, DIFF>(a); break;
+    case 4: if constexpr (M >= 5) tvs_bwd_level<DP, 5, INCR, RBF, DIFF>(a); break;
+    case 5: if constexpr (M >= 6) tvs_bwd_level<DP, 6, INCR, RBF, DIFF>(a); break;
+    case 6: if constexpr (M >= 7) tvs_bwd_level<DP, 7, INCR, RBF, DIFF>(a); break;
+    case 7: if constexpr (M >= 8) tvs_bwd_level<DP, 8, INCR, RBF, DIFF>(a); break;
     default: break;
   }
 }

@@ -7,7 +7,7 @@ namespace gpsig {
 size_t tvs_features_bytes(int n, int l, int d);
 int tvs_features_launch(const float *X, int n, int l, int d, float *Ft, hipStream_t s);
 template <int DP, bool INCR>
-int tvs_bwd_launch_dp(const TvsBwdArgs &a, int M, bool rbf, hipStream_t s);
+int tvs_bwd_launch_dp(const TvsBwdArgs &a, int M, bool rbf, bool diff, hipStream_t s);
 
 // gX[seq][s][q] += gXt[(s * d + q) * n + seq]
 __global__ __launch_bounds__(256) void tvs_gx_add_kernel(const float *__restrict__ gXt, int n, int l, int d,
@@ -31,10 +31,12 @@ extern "C" size_t gpsig_tens_vjp_workspace_bytes(int n, int l, int d) {
 }
 
 extern "C" int gpsig_tens_vs_seq_vjp(const float *Z, int lt, int t, int increments, int d, const float *X, int n,
-                                     int l, int num_levels, int base_kind, const float *gout, float *gZ, float *gX,
+                                     int l, int num_levels, int base_kind, int difference, const float *gout,
+                                     float *gZ, float *gX,
                                      void *workspace, size_t workspace_bytes, gpsig_stream_t stream) {
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (!Z || !X || !gout || !gZ || !gX || lt <= 0 || t <= 0 || n <= 0 || d <= 0 || l < 2 || num_levels < 1)
+  if (!Z || !X || !gout || !gZ || !gX || lt <= 0 || t <= 0 || n <= 0 || d <= 0 || l < (difference ? 2 : 1) ||
+      num_levels < 1)
     return GPSIG_EINVAL;
   if (lt != num_levels * (num_levels + 1) / 2) return GPSIG_EINVAL;
   if (base_kind != GPSIG_BASE_RBF && base_kind != GPSIG_BASE_LINEAR) return GPSIG_EUNSUPPORTED;
@@ -49,14 +51,14 @@ extern "C" int gpsig_tens_vs_seq_vjp(const float *Z, int lt, int t, int incremen
   TvsBwdArgs a{Z, Ft, t, n, l, d, gout, gZ, gXt};
   const bool rbf = base_kind == GPSIG_BASE_RBF;
   switch (DP * 2 + (increments ? 1 : 0)) {
-    case 4: rc = tvs_bwd_launch_dp<2, false>(a, num_levels, rbf, s); break;
-    case 5: rc = tvs_bwd_launch_dp<2, true>(a, num_levels, rbf, s); break;
-    case 8: rc = tvs_bwd_launch_dp<4, false>(a, num_levels, rbf, s); break;
-    case 9: rc = tvs_bwd_launch_dp<4, true>(a, num_levels, rbf, s); break;
-    case 12: rc = tvs_bwd_launch_dp<6, false>(a, num_levels, rbf, s); break;
-    case 13: rc = tvs_bwd_launch_dp<6, true>(a, num_levels, rbf, s); break;
-    case 16: rc = tvs_bwd_launch_dp<8, false>(a, num_levels, rbf, s); break;
-    case 17: rc = tvs_bwd_launch_dp<8, true>(a, num_levels, rbf, s); break;
+    case 4: rc = tvs_bwd_launch_dp<2, false>(a, num_levels, rbf, difference != 0, s); break;
+    case 5: rc = tvs_bwd_launch_dp<2, true>(a, num_levels, rbf, difference != 0, s); break;
+    case 8: rc = tvs_bwd_launch_dp<4, false>(a, num_levels, rbf, difference != 0, s); break;
+    case 9: rc = tvs_bwd_launch_dp<4, true>(a, num_levels, rbf, difference != 0, s); break;
+    case 12: rc = tvs_bwd_launch_dp<6, false>(a, num_levels, rbf, difference != 0, s); break;
+    case 13: rc = tvs_bwd_launch_dp<6, true>(a, num_levels, rbf, difference != 0, s); break;
+    case 16: rc = tvs_bwd_launch_dp<8, false>(a, num_levels, rbf, difference != 0, s); break;
+    case 17: rc = tvs_bwd_launch_dp<8, true>(a, num_levels, rbf, difference != 0, s); break;
     default: return GPSIG_EUNSUPPORTED;
   }
   if (rc) return rc;

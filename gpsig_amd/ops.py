@@ -341,8 +341,9 @@ def tens_vs_seq(Z: torch.Tensor, X: torch.Tensor, num_levels: int, order: int = 
 
 
 def tens_vs_seq_vjp(Z: torch.Tensor, X: torch.Tensor, num_levels: int, gout: torch.Tensor, base="rbf",
-                    increments: bool = False, gZ: torch.Tensor | None = None, gX: torch.Tensor | None = None):
-    """dLoss/dZ, dLoss/dX of the raw per-level tens_vs_seq output (order 1, difference=True) given
+                    increments: bool = False, gZ: torch.Tensor | None = None, gX: torch.Tensor | None = None,
+                    difference: bool = True):
+    """dLoss/dZ, dLoss/dX of the raw per-level tens_vs_seq output (order 1, difference True or False) given
     gout (num_levels+1, T, N); accumulated into float32 buffers (see gpsig_tens_vs_seq_vjp)."""
     _require_cuda(Z, X, gout)
     lib = L.load()
@@ -360,7 +361,8 @@ def tens_vs_seq_vjp(Z: torch.Tensor, X: torch.Tensor, num_levels: int, gout: tor
         gX = torch.zeros(X.shape, dtype=torch.float32, device=X.device)
     ws = workspace(X.device, lib.gpsig_tens_vjp_workspace_bytes(n, l, d))
     rc = lib.gpsig_tens_vs_seq_vjp(Z.data_ptr(), lt, t, int(increments), d, X.data_ptr(), n, l, num_levels,
-                                   base_kind(base), gout.data_ptr(), gZ.data_ptr(), gX.data_ptr(), ws.data_ptr(),
+                                   base_kind(base), int(bool(difference)), gout.data_ptr(), gZ.data_ptr(),
+                                   gX.data_ptr(), ws.data_ptr(),
                                    ws.numel(), _stream(X.device))
     L.check(rc, "gpsig_tens_vs_seq_vjp")
     return gZ, gX

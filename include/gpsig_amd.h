@@ -158,15 +158,15 @@ int gpsig_tens_gram(const float *Z, int lt, int t, int increments, int d, int nu
 int gpsig_tens_gram_vjp(const float *Z, int lt, int t, int increments, int d, int num_levels, int base_kind,
                         const float *gout, float *gZ, gpsig_stream_t stream);
 
-/* Gradient of gpsig_tens_vs_seq (order 1, difference = True, RBF or linear, num_levels <= 8, d <= 8):
+/* Gradient of gpsig_tens_vs_seq (order 1, difference 1 or 0, RBF or linear, num_levels <= 8, d <= 8):
  * the reference differentiates _K_tens_vs_seq (kernels.py:314-341 + signature_algs.py:101-127) by TF
  * autodiff.  gout (num_levels+1, T, n) = dLoss/d(raw per-level output); accumulates (+=) gZ (same
  * layout as Z) and gX (n, l, d).  Workspace: gpsig_tens_vjp_workspace_bytes(n, l, d). */
 size_t gpsig_tens_vjp_workspace_bytes(int n, int l, int d);
 
 int gpsig_tens_vs_seq_vjp(const float *Z, int lt, int t, int increments, int d, const float *X, int n, int l,
-                          int num_levels, int base_kind, const float *gout, float *gZ, float *gX, void *workspace,
-                          size_t workspace_bytes, gpsig_stream_t stream);
+                          int num_levels, int base_kind, int difference, const float *gout, float *gZ, float *gX,
+                          void *workspace, size_t workspace_bytes, gpsig_stream_t stream);
 
 size_t gpsig_rescaled_workspace_bytes(int n, int num_levels);
 

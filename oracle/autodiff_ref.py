@@ -125,11 +125,11 @@ def k_tens_vs_seq(Zs, Xs, num_levels, base="rbf", increments=False, difference=T
 
 
 def K_tens_vs_seq(Zs, Xs, num_levels, base="rbf", increments=False, normalization=True, scale=None, jitter=1e-6,
-                  return_levels=False):
+                  return_levels=False, difference=True):
     """SignatureKernel.K_tens_vs_seq (kernels.py:571-620) on scaled tensors / sequences."""
-    Kzx = k_tens_vs_seq(Zs, Xs, num_levels, base, increments)
+    Kzx = k_tens_vs_seq(Zs, Xs, num_levels, base, increments, difference)
     if normalization:
-        Kzx = Kzx / torch.sqrt(k_seq_diag(Xs, num_levels, base) + jitter)[:, None, :]
+        Kzx = Kzx / torch.sqrt(k_seq_diag(Xs, num_levels, base, difference) + jitter)[:, None, :]
     if scale is None:
         scale = torch.ones(num_levels + 1, dtype=Kzx.dtype)
     Kzx = Kzx * scale[:, None, None]

@@ -241,6 +241,32 @@ def test_autograd_state_budget(monkeypatch):
 
 @pytest.mark.parametrize("base", ["rbf", "linear"])
 @pytest.mark.parametrize("increments", [False, True])
+def test_tens_vs_seq_vjp_no_difference(base, increments):
+    """difference=False inducing-tensor kernel (point values as cells): Z and X gradients of the
+    normalised K_tens_vs_seq vs fp64 autodiff."""
+    import gpsig_amd
+    M, D, L, T, N = 4, 3, 17, 5, 67
+    LT = M * (M + 1) // 2
+    rng = np.random.default_rng(60)
+    Z = 0.5 * rng.standard_normal((LT, T, 2, D) if increments else (LT, T, D))
+    X = walks(N, L, D, 61)
+    G = rng.standard_normal((T, N))
+    cls = gpsig_amd.SignatureRBF if base == "rbf" else gpsig_amd.SignatureLinear
+    k = cls(L * D, D, M, difference=False)
+    Zt = torch.tensor(Z, device=DEV, requires_grad=True)
+    Xt = torch.tensor(X.reshape(N, -1), device=DEV, requires_grad=True)
+    K = k.K_tens_vs_seq(Zt, Xt, increments=increments)
+    (K * torch.as_tensor(G, device=DEV)).sum().backward()
+    Zr, Xr = torch.tensor(Z, requires_grad=True), torch.tensor(X, requires_grad=True)
+    Kr = ar.K_tens_vs_seq(Zr, Xr, M, base=base, increments=increments, difference=False)
+    (Kr * torch.tensor(G)).sum().backward()
+    assert norm_rel_err(K.detach().cpu().numpy(), Kr.detach().numpy()) < 1e-5
+    assert norm_rel_err(Zt.grad.cpu().numpy(), Zr.grad.numpy()) < GTOL
+    assert norm_rel_err(Xt.grad.reshape(X.shape).cpu().numpy(), Xr.grad.numpy()) < GTOL
+
+
+@pytest.mark.parametrize("base", ["rbf", "linear"])
+@pytest.mark.parametrize("increments", [False, True])
 @pytest.mark.parametrize("M,D,L", [(3, 3, 20), (5, 5, 40), (1, 2, 9), (8, 8, 12)])
 def test_tens_vs_seq_vjp_matches_autodiff(base, increments, M, D, L):
     """K_tens_vs_seq (normalised, summed) gradients in Z, X, lengthscales, variances."""
