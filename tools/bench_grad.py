@@ -4,7 +4,7 @@ device-synchronised calls, inputs resident), with the gradient's error vs torch 
 reference graph (oracle/autodiff_ref.py) / the reference's PDE adjoint (oracle/pde_grad.py) on a
 subsample.  One JSON object per line.
 
-    python tools/bench_grad.py [--only gram,kuf,pde,sig]
+    python tools/bench_grad.py [--only gram,kuf,kuf_incr,pde,pde_gram,sig]
 """
 import argparse
 import json
@@ -127,6 +127,33 @@ def bench_pde(reps, n=1024, l=200, d=5, dyadic=1):
                 fwd_ms=tf * 1e3, fwd_bwd_ms=tb * 1e3, grad_err=rel(Xs.grad.reshape(ref.shape).cpu().numpy(), ref))
 
 
+def bench_pde_gram(reps, n=256, l=100, d=5, dyadic=1):
+    """PDE cross Gram K(X, X2) (new in this build; the reference has only Kdiag) and its VJP."""
+    import gpsig_amd
+    from oracle import pde_grad
+    Xnp, Ynp = walks(n, l, d, 0), walks(n, l, d, 1)
+    X = torch.tensor(Xnp.reshape(n, -1), device="cuda", dtype=torch.float32)
+    Y = torch.tensor(Ynp.reshape(n, -1), device="cuda", dtype=torch.float32)
+    G = torch.randn(n, n, device="cuda")
+    k = gpsig_amd.UntruncSignatureKernel(l * d, d, order=dyadic)
+
+    def fwd():
+        with torch.no_grad():
+            k.K(X, Y)
+
+    def fb():
+        Xg = X.detach().requires_grad_(True)
+        (k.K(Xg, Y) * G).sum().backward()
+
+    tf, tb = timed(fwd, reps), timed(fb, reps)
+    Xs = torch.tensor(Xnp[:1].reshape(1, -1), device="cuda", requires_grad=True)
+    Ys = torch.tensor(Ynp[:1].reshape(1, -1), device="cuda")
+    k.K(Xs, Ys).sum().backward()
+    ref, _ = pde_grad.pair_grad(Xnp[0], Ynp[0], dyadic)
+    return dict(path="pde_gram", workload=f"UntruncSignatureKernel K(X, X2) N={n}x{n} L={l} D={d} dyadic={dyadic} (dX)",
+                fwd_ms=tf * 1e3, fwd_bwd_ms=tb * 1e3, grad_err=rel(Xs.grad.reshape(ref.shape).cpu().numpy(), ref))
+
+
 def bench_sig(reps, n=4096, l=100, d=5, depth=3):
     from gpsig_amd import signatures as sg
     from oracle import autodiff_ref as ar
@@ -156,11 +183,12 @@ def bench_sig(reps, n=4096, l=100, d=5, depth=3):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--only", default="gram,kuf,kuf_incr,pde,sig")
+    ap.add_argument("--only", default="gram,kuf,kuf_incr,pde,pde_gram,sig")
     a = ap.parse_args()
     todo = a.only.split(",")
     runs = dict(gram=lambda: bench_gram(a.reps), kuf=lambda: bench_kuf(a.reps),
                 kuf_incr=lambda: bench_kuf(a.reps, increments=True), pde=lambda: bench_pde(a.reps),
+                pde_gram=lambda: bench_pde_gram(a.reps),
                 sig=lambda: bench_sig(a.reps))
     for name in todo:
         r = runs[name]()
