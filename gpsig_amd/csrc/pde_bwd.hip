@@ -27,7 +27,8 @@ struct PdeBwdArgs {
   int ntb, tiles_a0;
   const float *gout;  // DIAG: (n1,); RECT: (n1, n2)
   float *gX, *gY;     // accumulated (n1, l1, d), (n2, l2, d)
-  double *grid;       // scratch: (row_end - row_begin) * [n2 | 1] grids of (I+1) x (J+1)
+  double *grid;       // scratch: per evaluated pair, the interior K_rev cells in wavefront-step order
+                      // (pde_grid_cells: steps x lanes x W doubles)
 };
 
 template <int DP, int W, bool REV, bool COLS>
@@ -55,7 +56,11 @@ __global__ __launch_bounds__(256) void pde_bwd_kernel(PdeBwdArgs p) {
   const float *x = p.X + (long long)a * p.l1 * d;
   const float *y = p.Y + (long long)b * p.l2 * d;
   const long long pidx = diag ? (long long)(a - p.row_begin) : (long long)(a - p.row_begin) * p.n2 + b;
-  double *grid = p.grid + pidx * (long long)(I + 1) * (J + 1);
+  const int lanes_used = (J + W - 1) / W;
+  // K_rev cell (i, c) (interior, 0-based) was produced at wavefront step i + c / W by lane c / W:
+  // stored at [(i + c/W) * lanes_used + c/W] * W + c % W, so each step's cells are one contiguous
+  // block (coalesced stores) and the reversed read of the GRAD pass touches one or two blocks per step
+  double *grid = p.grid + pidx * (long long)(I + lanes_used - 1) * lanes_used * W;
 
   // LDS: [wave] { dx (IC x DP floats, as doubles' storage) | row accumulators (IC x DP doubles) }
   double *wl = ldsd + (size_t)wave * IC * DP * 2;
@@ -78,11 +83,6 @@ __global__ __launch_bounds__(256) void pde_bwd_kernel(PdeBwdArgs p) {
 #pragma unroll
     for (int k = 0; k < DP; ++k) dy[w][k] = k < d ? y[(cj + 1) * d + k] - y[cj * d + k] : 0.0f;
   }
-  if (REV) {
-    // boundaries of the stored grid
-    for (int c = lane; c <= J; c += 64) grid[c] = 1.0;
-    for (int r = lane; r <= I; r += 64) grid[(long long)r * (J + 1)] = 1.0;
-  }
   __syncthreads();
 
   const int solver = REV ? 0 : p.solver;
@@ -96,7 +96,6 @@ __global__ __launch_bounds__(256) void pde_bwd_kernel(PdeBwdArgs p) {
     for (int k = 0; k < DP; ++k) gcol[w][k] = 0.0;
   }
   double last = 1.0, left_prev = 1.0;
-  const int lanes_used = (J + W - 1) / W;
   const int nsteps = ok ? I + lanes_used - 1 : 0;  // invalid waves still reach the barrier below
   for (int s = 0; s < nsteps; ++s) {
     double left = lane_prev(last);
@@ -113,14 +112,21 @@ __global__ __launch_bounds__(256) void pde_bwd_kernel(PdeBwdArgs p) {
       double grow[DP];
 #pragma unroll
       for (int k = 0; k < DP; ++k) grow[k] = 0.0;
-      // K_rev[I-1-i][J-1-c] of the lane's columns, loaded before the column loop
+      // K_rev[I-1-i][J-1-c] (grid indices, boundary row / column = 1) of the lane's columns, loaded
+      // before the column loop: interior cell (I-2-i, J-2-c)
       double kr[W];
       if constexpr (!REV) {
-        const double *krr = p.grid + pidx * (long long)(I + 1) * (J + 1) + (long long)(I - 1 - i) * (J + 1) + (J - 1);
+        const int ir = I - 2 - i;
 #pragma unroll
         for (int w = 0; w < W; ++w) {
           const int c = lane * W + w;
-          kr[w] = c < J ? krr[-c] : 0.0;
+          const int cr = J - 2 - c;
+          double v = 1.0;
+          if (ir >= 0 && cr >= 0) {
+            const int lr = cr / W;
+            v = grid[((long long)(ir + lr) * lanes_used + lr) * W + (cr - lr * W)];
+          }
+          kr[w] = c < J ? v : 0.0;
         }
       }
 #pragma unroll
@@ -140,7 +146,7 @@ __global__ __launch_bounds__(256) void pde_bwd_kernel(PdeBwdArgs p) {
         }
         if (c < J) {
           if (REV) {
-            grid[(long long)(i + 1) * (J + 1) + c + 1] = kn;
+            grid[((long long)s * lanes_used + lane) * W + w] = kn;  // cell (i, c), step s = i + lane
           } else {
             // KK[i][c] = K[i][c] * K_rev[I-1-i][J-1-c]
             const double kk = cor * kr[w];
@@ -225,9 +231,18 @@ static int pde_bwd_w(const PdeBwdArgs &a, long long nblocks, int J, hipStream_t 
 
 using namespace gpsig;
 
-extern "C" size_t gpsig_pde_vjp_workspace_bytes(int npairs, int l1, int l2, int dyadic) {
+// Interior K_rev cells of one pair in wavefront-step order (pde_bwd_kernel): (I + lanes - 1) steps x
+// lanes x W, with W the launch's columns per lane (pde_bwd_w) and lanes = ceil(J / W).
+static long long pde_grid_cells(int l1, int l2, int dyadic) {
   const long long I = (long long)(1 << dyadic) * (l1 - 1), J = (long long)(1 << dyadic) * (l2 - 1);
-  return (size_t)npairs * (size_t)((I + 1) * (J + 1)) * sizeof(double);
+  const long long W = J <= 64 ? 1 : J <= 128 ? 2 : J <= 256 ? 4 : J <= 512 ? 8 : 16;
+  const long long lanes = (J + W - 1) / W;
+  return (I + lanes - 1) * lanes * W;
+}
+
+extern "C" size_t gpsig_pde_vjp_workspace_bytes(int npairs, int l1, int l2, int dyadic) {
+  if (npairs <= 0 || l1 < 2 || l2 < 2 || dyadic < 0 || dyadic > 6) return 0;
+  return (size_t)npairs * (size_t)pde_grid_cells(l1, l2, dyadic) * sizeof(double);
 }
 
 extern "C" int gpsig_pde_vjp(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int dyadic,

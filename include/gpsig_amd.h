@@ -193,8 +193,9 @@ int gpsig_pde_diag(const float *X, int n, int l, int d, int dyadic, int solver, 
  * _KdiagGrad; covariance_op/_untrunc_cov_grad.py:25-77): KK = K (.) flip(K_rev) with K_rev solved on the
  * time-reversed paths by the first-order scheme, contracted with the increments.  pair_mode DIAG
  * (gout (n1,), dLoss/dk(x_a, x_a); the reference's factor 2 for the symmetric pair) or RECT (gout
- * (n1, n2); gX and gY).  Accumulates (+=) gX (n1, l1, d), gY (n2, l2, d).  Workspace: one fp64
- * (2^dyadic (l1-1) + 1) x (2^dyadic (l2-1) + 1) grid per evaluated pair,
+ * (n1, n2); gX and gY).  Accumulates (+=) gX (n1, l1, d), gY (n2, l2, d).  Workspace: the fp64
+ * K_rev cells of each evaluated pair in the solver's wavefront order (about (I + J/W) J doubles,
+ * I = 2^dyadic (l1-1), J = 2^dyadic (l2-1)),
  * gpsig_pde_vjp_workspace_bytes(pairs, l1, l2, dyadic). */
 size_t gpsig_pde_vjp_workspace_bytes(int npairs, int l1, int l2, int dyadic);
 

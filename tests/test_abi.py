@@ -83,7 +83,7 @@ def test_vjp_and_feature_entry_points_validate_arguments():
     assert lib.gpsig_signature(None, 4, 10, 3, 3, None, None) == L.GPSIG_EINVAL
     assert lib.gpsig_signature_vjp(None, 4, 10, 3, 3, None, None, None) == L.GPSIG_EINVAL
     assert lib.gpsig_signature_channels(5, 3) == 5 + 25 + 125
-    assert lib.gpsig_pde_vjp_workspace_bytes(2, 10, 10, 1) == 2 * 19 * 19 * 8
+    assert lib.gpsig_pde_vjp_workspace_bytes(2, 10, 10, 1) == 2 * (18 + 18 - 1) * 18 * 8  # W = 1: 18 lanes
 
 
 def test_graph_capture_refuses_host_tensors_and_kernel_to():
