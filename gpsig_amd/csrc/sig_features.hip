@@ -72,6 +72,8 @@ __global__ __launch_bounds__(256) void sig_features_kernel(SigFeatArgs a) {
 //   dS_j[u]  = sum_{m>=j} sum_v dT_m[u v] E_{m-j}[v]          (in place, ascending j)
 //   dh[q]    = sum_r sum_v dE_r[v] dE_r[v]/dh[q],  E_r[v] = h[v_1] ... h[v_r] / r!
 // and dx_{k+1} += dh, dx_k -= dh.  LDS: h, dh, S, dS, dE.
+constexpr int GH_REG = 8;  // channels whose increment gradient is accumulated in registers
+
 __global__ __launch_bounds__(256) void sig_features_bwd_kernel(SigFeatArgs a, const float *__restrict__ gout,
                                                                float *__restrict__ gX) {
   extern __shared__ __attribute__((aligned(16))) float sh[];
@@ -153,7 +155,11 @@ __global__ __launch_bounds__(256) void sig_features_bwd_kernel(SigFeatArgs a, co
         gE[off[r] + v] = acc;
       }
     __syncthreads();
-    // dh from dE (LDS float atomics into d slots)
+    // dh from dE: per-thread partials in registers (d <= GH_REG), reduced over the wave and added
+    // to the d LDS slots by one lane per wave; wider paths take LDS atomics
+    float ghr[GH_REG];
+#pragma unroll
+    for (int q = 0; q < GH_REG; ++q) ghr[q] = 0.0f;
     for (int r = 1; r <= M; ++r)
       for (int v = tid; v < sz[r]; v += nth) {
         const float ge = gE[off[r] + v];
@@ -170,9 +176,22 @@ __global__ __launch_bounds__(256) void sig_features_bwd_kernel(SigFeatArgs a, co
             if (p2 != p) P *= h[w % d];
             w /= d;
           }
-          atomicAdd(gh + q, ge * P / fact);
+          const float val = ge * P / fact;
+          if (d <= GH_REG) {
+#pragma unroll
+            for (int q2 = 0; q2 < GH_REG; ++q2) ghr[q2] += (q2 == q) ? val : 0.0f;  // no dynamic register index
+          } else {
+            atomicAdd(gh + q, val);
+          }
         }
       }
+    if (d <= GH_REG) {
+      group_incl_scan_n<64, GH_REG>(ghr);  // wave sums in lane 63
+      if ((tid & 63) == 63)
+#pragma unroll
+        for (int q = 0; q < GH_REG; ++q)
+          if (q < d) atomicAdd(gh + q, ghr[q]);
+    }
     // dS_j[u] = sum_{m>=j} sum_v dT_m[u v] E_{m-j}[v], ascending j in place
     for (int j = 1; j <= M; ++j) {
       for (int u = tid; u < sz[j]; u += nth) {
