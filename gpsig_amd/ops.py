@@ -46,6 +46,14 @@ def workspace(device, nbytes: int) -> torch.Tensor:
         return buf
 
 
+def release_workspaces() -> None:
+    """Drop the cached per-stream scratch buffers (feature records, the PDE VJP's K_rev cells -- up to
+    PDE_VJP_SCRATCH bytes); the next call allocates again.  Not to be called while a captured graph
+    that uses them (gpsig_amd.graphs) may still replay."""
+    with _ws_lock:
+        _ws.clear()
+
+
 def base_kind(base) -> int:
     if isinstance(base, int):
         return base

@@ -98,3 +98,10 @@ def test_graph_capture_refuses_host_tensors_and_kernel_to():
     k.to("cpu")
     assert k.lengthscales.is_leaf and k.lengthscales.requires_grad
     assert gpsig_amd.UntruncSignatureKernel(20, 2).to("cpu").num_features == 2
+
+
+def test_release_workspaces_clears_cache():
+    from gpsig_amd import ops
+    ops._ws[("x", 0)] = object()
+    ops.release_workspaces()
+    assert not ops._ws
