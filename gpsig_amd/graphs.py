@@ -39,6 +39,11 @@ class GraphedCall:
         self.graph = torch.cuda.CUDAGraph()
         with torch.no_grad(), torch.cuda.graph(self.graph, stream=self.stream):
             self.static_out = fn(*self.static_in)
+        # the captured launches address the per-stream scratch buffers: hold them for the graph's
+        # lifetime (gpsig_amd.ops.release_workspaces() only drops the cache's references)
+        from . import ops
+        with ops._ws_lock:
+            self._scratch = list(ops._ws.values())
 
     def __call__(self, *inputs):
         if len(inputs) != len(self.static_in):

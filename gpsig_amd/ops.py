@@ -48,8 +48,8 @@ def workspace(device, nbytes: int) -> torch.Tensor:
 
 def release_workspaces() -> None:
     """Drop the cached per-stream scratch buffers (feature records, the PDE VJP's K_rev cells -- up to
-    PDE_VJP_SCRATCH bytes); the next call allocates again.  Not to be called while a captured graph
-    that uses them (gpsig_amd.graphs) may still replay."""
+    PDE_VJP_SCRATCH bytes); the next call allocates again.  Captured graphs (gpsig_amd.graphs) keep
+    their own references to the buffers they address."""
     with _ws_lock:
         _ws.clear()
 
