@@ -59,3 +59,21 @@ def test_graphed_call_rejects_shape_change():
     g = GraphedCall(lambda a: k.K(a), X)
     with pytest.raises(ValueError):
         g(torch.zeros(5, 20, device=DEV))
+
+
+def test_graph_survives_workspace_release():
+    """The captured launches keep addressing valid scratch after ops.release_workspaces()."""
+    import gpsig_amd
+    from gpsig_amd import ops
+    from gpsig_amd.graphs import GraphedCall
+    N, L, D, M = 32, 40, 3, 4
+    k = gpsig_amd.SignatureRBF(L * D, D, M).to(DEV)
+    X0 = torch.tensor(walks(N, L, D, 7).reshape(N, -1), device=DEV, dtype=torch.float32)
+    g = GraphedCall(lambda X: k.K(X), X0)
+    ops.release_workspaces()
+    junk = [torch.full((1 << 20,), 7.0, device=DEV) for _ in range(8)]  # reuse of freed blocks, if any
+    X1 = torch.tensor(walks(N, L, D, 8).reshape(N, -1), device=DEV, dtype=torch.float32)
+    got = g(X1).clone()
+    with torch.no_grad():
+        assert torch.equal(got, k.K(X1))
+    del junk
