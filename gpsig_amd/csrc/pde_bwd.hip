@@ -57,10 +57,13 @@ __global__ __launch_bounds__(256) void pde_bwd_kernel(PdeBwdArgs p) {
   const float *y = p.Y + (long long)b * p.l2 * d;
   const long long pidx = diag ? (long long)(a - p.row_begin) : (long long)(a - p.row_begin) * p.n2 + b;
   const int lanes_used = (J + W - 1) / W;
-  // K_rev cell (i, c) (interior, 0-based) was produced at wavefront step i + c / W by lane c / W:
-  // stored at [(i + c/W) * lanes_used + c/W] * W + c % W, so each step's cells are one contiguous
-  // block (coalesced stores) and the reversed read of the GRAD pass touches one or two blocks per step
-  double *grid = p.grid + pidx * (long long)(I + lanes_used - 1) * lanes_used * W;
+  // STEP (W < 8): K_rev cell (i, c) (interior, 0-based) was produced at wavefront step i + c / W by
+  // lane c / W: stored at [(i + c/W) * lanes_used + c/W] * W + c % W, so each step's cells are one
+  // contiguous block (coalesced stores) and the reversed read of the GRAD pass touches one or two
+  // blocks per step.  W >= 8: the (I+1) x (J+1) row-major grid with its boundary row / column (each
+  // lane's run is already 64 bytes, and it has no step padding).
+  constexpr bool STEP = W < 8;
+  double *grid = p.grid + pidx * (STEP ? (long long)(I + lanes_used - 1) * lanes_used * W : (long long)(I + 1) * (J + 1));
 
   // LDS: [wave] { dx (IC x DP floats, as doubles' storage) | row accumulators (IC x DP doubles) }
   double *wl = ldsd + (size_t)wave * IC * DP * 2;
@@ -82,6 +85,11 @@ __global__ __launch_bounds__(256) void pde_bwd_kernel(PdeBwdArgs p) {
     if (REV) cj = JC - 1 - cj;
 #pragma unroll
     for (int k = 0; k < DP; ++k) dy[w][k] = k < d ? y[(cj + 1) * d + k] - y[cj * d + k] : 0.0f;
+  }
+  if (REV && !STEP) {
+    // boundaries of the stored grid
+    for (int c = lane; c <= J; c += 64) grid[c] = 1.0;
+    for (int r = lane; r <= I; r += 64) grid[(long long)r * (J + 1)] = 1.0;
   }
   __syncthreads();
 
@@ -116,17 +124,26 @@ __global__ __launch_bounds__(256) void pde_bwd_kernel(PdeBwdArgs p) {
       // before the column loop: interior cell (I-2-i, J-2-c)
       double kr[W];
       if constexpr (!REV) {
-        const int ir = I - 2 - i;
+        if constexpr (STEP) {
+          const int ir = I - 2 - i;
 #pragma unroll
-        for (int w = 0; w < W; ++w) {
-          const int c = lane * W + w;
-          const int cr = J - 2 - c;
-          double v = 1.0;
-          if (ir >= 0 && cr >= 0) {
-            const int lr = cr / W;
-            v = grid[((long long)(ir + lr) * lanes_used + lr) * W + (cr - lr * W)];
+          for (int w = 0; w < W; ++w) {
+            const int c = lane * W + w;
+            const int cr = J - 2 - c;
+            double v = 1.0;
+            if (ir >= 0 && cr >= 0) {
+              const int lr = cr / W;
+              v = grid[((long long)(ir + lr) * lanes_used + lr) * W + (cr - lr * W)];
+            }
+            kr[w] = c < J ? v : 0.0;
           }
-          kr[w] = c < J ? v : 0.0;
+        } else {
+          const double *krr = grid + (long long)(I - 1 - i) * (J + 1) + (J - 1);
+#pragma unroll
+          for (int w = 0; w < W; ++w) {
+            const int c = lane * W + w;
+            kr[w] = c < J ? krr[-c] : 0.0;
+          }
         }
       }
 #pragma unroll
@@ -146,7 +163,10 @@ __global__ __launch_bounds__(256) void pde_bwd_kernel(PdeBwdArgs p) {
         }
         if (c < J) {
           if (REV) {
-            grid[((long long)s * lanes_used + lane) * W + w] = kn;  // cell (i, c), step s = i + lane
+            if constexpr (STEP)
+              grid[((long long)s * lanes_used + lane) * W + w] = kn;  // cell (i, c), step s = i + lane
+            else
+              grid[(long long)(i + 1) * (J + 1) + c + 1] = kn;
           } else {
             // KK[i][c] = K[i][c] * K_rev[I-1-i][J-1-c]
             const double kk = cor * kr[w];
@@ -231,11 +251,13 @@ static int pde_bwd_w(const PdeBwdArgs &a, long long nblocks, int J, hipStream_t 
 
 using namespace gpsig;
 
-// Interior K_rev cells of one pair in wavefront-step order (pde_bwd_kernel): (I + lanes - 1) steps x
-// lanes x W, with W the launch's columns per lane (pde_bwd_w) and lanes = ceil(J / W).
+// K_rev cells of one pair (pde_bwd_kernel): W < 8 (W = the launch's columns per lane, pde_bwd_w) the
+// wavefront-step order, (I + lanes - 1) steps x lanes x W with lanes = ceil(J / W); else the
+// (I+1) x (J+1) grid.
 static long long pde_grid_cells(int l1, int l2, int dyadic) {
   const long long I = (long long)(1 << dyadic) * (l1 - 1), J = (long long)(1 << dyadic) * (l2 - 1);
   const long long W = J <= 64 ? 1 : J <= 128 ? 2 : J <= 256 ? 4 : J <= 512 ? 8 : 16;
+  if (W >= 8) return (I + 1) * (J + 1);
   const long long lanes = (J + W - 1) / W;
   return (I + lanes - 1) * lanes * W;
 }
