@@ -194,8 +194,8 @@ int gpsig_pde_diag(const float *X, int n, int l, int d, int dyadic, int solver, 
  * time-reversed paths by the first-order scheme, contracted with the increments.  pair_mode DIAG
  * (gout (n1,), dLoss/dk(x_a, x_a); the reference's factor 2 for the symmetric pair) or RECT (gout
  * (n1, n2); gX and gY).  Accumulates (+=) gX (n1, l1, d), gY (n2, l2, d).  Workspace: the fp64
- * K_rev cells of each evaluated pair in the solver's wavefront order (about (I + J/W) J doubles,
- * I = 2^dyadic (l1-1), J = 2^dyadic (l2-1)),
+ * K_rev cells of each evaluated pair (the (I+1) x (J+1) grid, or for J <= 256 the solver's
+ * wavefront order, about (I + J/W) J doubles; I = 2^dyadic (l1-1), J = 2^dyadic (l2-1)),
  * gpsig_pde_vjp_workspace_bytes(pairs, l1, l2, dyadic). */
 size_t gpsig_pde_vjp_workspace_bytes(int npairs, int l1, int l2, int dyadic);
 
