@@ -62,18 +62,35 @@ def _cpu_worker(args):
     return done, time.perf_counter() - t0
 
 
-def cpu_baseline(l, d, m, seconds=15.0, n_blk=8):
+def _cpu_model():
     try:
-        cores = len(os.sched_getaffinity(0))
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:  # pragma: no cover
+        pass
+    return "unknown"
+
+
+def cpu_baseline(l, d, m, seconds=15.0, n_blk=8):
+    """The fp64 NumPy restatement of the reference dataflow, one single-threaded process per core.
+    Cores: every CPU in the affinity mask, capped at the CPU share the job is given (OMP_NUM_THREADS,
+    16 on the GPU boxes, whose affinity mask shows the whole host)."""
+    try:
+        affinity = len(os.sched_getaffinity(0))
     except AttributeError:  # pragma: no cover
-        cores = os.cpu_count() or 1
-    procs = max(1, min(16, cores))
+        affinity = os.cpu_count() or 1
+    share = int(os.environ.get("OMP_NUM_THREADS", affinity) or affinity)
+    procs = max(1, min(affinity, share))
     with mp.get_context("spawn").Pool(procs) as pool:
         res = pool.map(_cpu_worker, [(seconds, n_blk, l, d, m, 100 + i) for i in range(procs)])
     entries = sum(r[0] for r in res)
     wall = max(r[1] for r in res)
-    return dict(value=entries / wall, unit="entries/s", cores=procs, kind="port",
-                sample=(f"{procs} processes x {wall:.1f}s of {n_blk}x{n_blk}-pair raw per-level Gram blocks, "
+    return dict(value=entries / wall, unit="entries/s", cores=procs, affinity_cores=affinity,
+                cpu_model=_cpu_model(), kind="port",
+                sample=(f"{procs} single-threaded processes (one per core of the job's CPU share; affinity "
+                        f"mask {affinity}) x {wall:.1f}s of {n_blk}x{n_blk}-pair raw per-level Gram blocks, "
                         f"L={l}, D={d}, M={m}: oracle/kernels_ref.py float64 NumPy restatement of the "
                         f"reference dataflow (materialised base-kernel tensor, exclusive cumsums)"))
 
@@ -109,6 +126,8 @@ def main():
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-check", action="store_true")
     ap.add_argument("--no-probe", action="store_true", help="skip the HBM copy-bandwidth probe")
+    ap.add_argument("--seed-engine", default="valu", choices=["valu", "mfma"],
+                    help="RBF seed dots on packed VALU FMAs (default) or on the matrix cores (A/B arm)")
     ap.add_argument("--backend", default="nccl",
                     help="process-group backend (nccl = RCCL; gloo only to rehearse N>1 ranks on one GPU)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r1_gram_counters.json"),
@@ -152,15 +171,19 @@ def main():
         r = ops.sig_gram(Xs, None, rows=rows, out=out, out_row0=out_row0, **kw)
         e1.record()
         ev.append((e0, e1))
-        rows_done[0] += rows[1] - rows[0]
+        # pairs the launch evaluates: symmetric K(X) computes b >= a only (the mirror is a store)
+        a0, a1 = rows
+        rows_done[0] += (a1 - a0) * n - (a1 * (a1 - 1) - a0 * (a0 - 1)) // 2
         return r
+
+    gram_base = L.BASE_RBF | (L.BASE_SEED_MFMA if args.seed_engine == "mfma" else 0)
 
     def step():
         Xs = kern._prep(X)
         rs = kern._rsqrt_diag(Xs)
         return gdist.sharded_sym_gram(Xs, m, out_mode=L.OUT_NORM_SUM, compute=timed_compute, rs1=rs, rs2=rs,
                                       scale=kern._scale_vec(dev), jitter=kern.jitter, order=kern.order,
-                                      base=kern.base, difference=kern.difference)
+                                      base=gram_base, difference=kern.difference)
 
     for _ in range(args.warmup):
         K = step()
@@ -185,7 +208,7 @@ def main():
     # dominant-kernel roofline: algorithmic bytes per Gram entry
     kern_ms = sum(a.elapsed_time(b) for a, b in ev)
     launches = len(ev)
-    entries_per_launch = rows_done[0] * n / max(launches, 1)
+    entries_per_launch = rows_done[0] / max(launches, 1)  # evaluated (upper-triangle) pairs
     b_entry = 4 * (l - 1) * (l - 1) + 4 * (m + 1)
     avg_launch_s = kern_ms / 1e3 / max(launches, 1)
     achieved = entries_per_launch * b_entry / avg_launch_s / 1e9
@@ -215,7 +238,7 @@ def main():
                    "global_batch": n, "seq_len": l, "parallelism": f"row-shard{world}" if world > 1 else "single"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "sig_fo_kernel", "launch_ms": avg_launch_s * 1e3, "bytes_per_entry": b_entry,
+                     "kernel": "sig_fo_kernel", "seed_engine": args.seed_engine, "launch_ms": avg_launch_s * 1e3, "bytes_per_entry": b_entry,
                      "entries_per_launch": entries_per_launch,
                      # the fused kernel never materialises the tile: physically it is VALU-issue bound
                      "physical_bound": "valu", "valu_issue_util": prof.get("valu_issue_util"),

@@ -33,6 +33,7 @@ _ERRORS = {
 
 BASE_RBF = 0
 BASE_LINEAR = 1
+BASE_SEED_MFMA = 0x100  # flag: RBF seed dots on the matrix cores (A/B arm, include/gpsig_amd.h)
 PAIRS_RECT, PAIRS_UPPER, PAIRS_DIAG = 0, 1, 2
 OUT_LEVELS, OUT_NORM_LEVELS, OUT_NORM_SUM, OUT_RSQRT = 0, 1, 2, 3
 

@@ -5,7 +5,7 @@
 namespace gpsig {
 int features(const float *X, int n, int l, int d, int DP, float *F, hipStream_t s);
 int sig_fo_launch(const SigArgs &a, int DP, int seed, long long nblocks, hipStream_t s);
-int fo_lanes_per_pair(int l2, int DP, int M);
+int fo_lanes_per_pair(int l2, int DP, int M, bool mf);
 int sig_ho_launch(const SigArgs &a, int DP, int seed, long long nblocks, hipStream_t s);
 int ho_lanes_per_pair(int l2, int order, int M);
 int pde_launch(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int dyadic, int solver,
@@ -63,7 +63,10 @@ static int sig_gram_impl(const float *X, int n1, int l1, const float *Y, int n2,
   if (out_mode == GPSIG_OUT_RSQRT && pair_mode != GPSIG_PAIRS_DIAG) return GPSIG_EINVAL;
   if ((rs1 == nullptr) != (rs2 == nullptr)) return GPSIG_EINVAL;
   if (order < 1) return GPSIG_EINVAL;
+  const bool mfma = (base_kind & GPSIG_BASE_SEED_MFMA) != 0;
+  base_kind &= ~GPSIG_BASE_SEED_MFMA;
   const int seed = seed_of(base_kind, difference);
+  if (mfma && (seed != SEED_RBF_DIFF || order != 1 || state)) return GPSIG_EUNSUPPORTED;
   const int DP = pad_channels(d, order);
   if (seed < 0 || DP == 0) return GPSIG_EUNSUPPORTED;
   if (row_end == row_begin) return GPSIG_OK;
@@ -97,8 +100,9 @@ static int sig_gram_impl(const float *X, int n1, int l1, const float *Y, int n2,
   a.out_ld = n2;
   a.out_lvl = (long long)out_rows * n2;
   a.state = state;
+  a.mfma = mfma ? 1 : 0;
 
-  const int LP = (order == 1) ? fo_lanes_per_pair(l2, DP, num_levels) : ho_lanes_per_pair(l2, order, num_levels);
+  const int LP = (order == 1) ? fo_lanes_per_pair(l2, DP, num_levels, mfma) : ho_lanes_per_pair(l2, order, num_levels);
   if (LP == 0) return GPSIG_EUNSUPPORTED;
   const int G = 64 / LP;
   long long nblocks = 0;

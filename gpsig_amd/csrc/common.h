@@ -112,6 +112,7 @@ GPSIG_DEV float em1_small(float x) {
 // per lane in one VALU issue (a wave-uniform SGPR operand is broadcast through op_sel), so every
 // per-cell evaluation is written on column pairs.
 typedef float f2 __attribute__((ext_vector_type(2)));
+typedef float f4 __attribute__((ext_vector_type(4)));
 GPSIG_DEV f2 splat2(float v) { return (f2){v, v}; }
 GPSIG_DEV f2 fma2(f2 a, f2 b, f2 c) { return __builtin_elementwise_fma(a, b, c); }
 GPSIG_DEV f2 em1_small2(f2 x) {

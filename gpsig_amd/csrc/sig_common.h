@@ -35,6 +35,7 @@ struct SigArgs {
   int out_row0, out_rows;
   long long out_ld, out_lvl;  // row stride, level stride (elements)
   float *state;               // optional saved forward state for the VJP (gpsig_sig_gram_state)
+  int mfma;                   // RBF difference seed: increment dots on the matrix cores (GPSIG_BASE_SEED_MFMA)
 };
 
 // Saved forward state of a first-order pair (gpsig_sig_gram_state): column sums of levels 1..M-1
@@ -310,7 +311,7 @@ struct RbfSeedPk {
   // Cells of row i into dM.  anch (wave-uniform): the next row's state is re-evaluated exactly
   // instead of by the recurrences.
   GPSIG_DEV void row(const Row &rd, bool anch, f2 (&dM)[W2]) {
-    f2 p[W2], c[W2], Eqn[W2], kn[W2];
+    f2 p[W2], c[W2];
 #pragma unroll
     for (int w2 = 0; w2 < W2; ++w2) {
       f2 a = splat2(-rd.g), cc = splat2(0.0f);
@@ -322,6 +323,40 @@ struct RbfSeedPk {
       p[w2] = a;
       c[w2] = cc;
     }
+    row_pc(rd, anch, p, c, dM);
+  }
+
+  // The increment inner products of 4 consecutive rows i0 .. i0+3 on the matrix cores
+  // (v_mfma_f32_4x4x1_16b_f32: 16 blocks of 4 x 4 outer products, one k per instruction).  Block b of
+  // the wave is lanes 4b .. 4b+3; the A operand of lane l is row i0 + (l & 3), the B operand is the
+  // lane's own column, and accumulator register r of lane l receives row i0 + r of column l:
+  //   P[w][r] = <y_j, dx_{i0+r}> - g_{i0+r},   Q[w][r] = <dy_j, dx_{i0+r}>,   j = column w of the lane
+  // (k-ordered fp32 fma chains, as the VALU dots).  The seed GEMM of the reference (kernels.py:946-957
+  // _square_dist -> tf.matmul) restricted to what the recursion consumes.
+  GPSIG_DEV void mfma_pc(const float *__restrict__ fx, int i0, f4 (&P)[W], f4 (&Q)[W]) const {
+    const float *__restrict__ fa = fx + (long long)(i0 + (int)(__lane_id() & 3)) * FS;
+    float ax[DP];
+#pragma unroll
+    for (int k = 0; k < DP; ++k) ax[k] = fa[DP + k];
+    const float ng = -fa[2 * DP + 1];
+    const f4 zero = {0.0f, 0.0f, 0.0f, 0.0f};
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      const int w2 = w % W2, h = w / W2;
+      f4 accp = __builtin_amdgcn_mfma_f32_4x4x1f32(ng, 1.0f, zero, 0, 0, 0);
+      f4 accq = __builtin_amdgcn_mfma_f32_4x4x1f32(ax[0], dy[w2][0][h], zero, 0, 0, 0);
+#pragma unroll
+      for (int k = 0; k < DP; ++k) accp = __builtin_amdgcn_mfma_f32_4x4x1f32(ax[k], y[w2][k][h], accp, 0, 0, 0);
+#pragma unroll
+      for (int k = 1; k < DP; ++k) accq = __builtin_amdgcn_mfma_f32_4x4x1f32(ax[k], dy[w2][k][h], accq, 0, 0, 0);
+      P[w] = accp;
+      Q[w] = accq;
+    }
+  }
+
+  // Cells of row i from its precomputed p, c (column pairs).
+  GPSIG_DEV void row_pc(const Row &rd, bool anch, const f2 (&p)[W2], const f2 (&c)[W2], f2 (&dM)[W2]) {
+    f2 Eqn[W2], kn[W2];
     f2 Ep[W2], Ec[W2];
     em1_small2_n<W2>(p, Ep);
     em1_small2_n<W2>(c, Ec);

@@ -21,7 +21,9 @@ namespace gpsig {
 // DIAGK: the diagonal pass (pairs (a, a)) is the same body under its own symbol, so profiler
 // statistics of the Gram launch are not mixed with it.  SAVE: also write the VJP's saved state
 // (gpsig_sig_gram_state) -- a separate instantiation, so the plain Gram keeps its register budget.
-template <int DP, int W, int LP, int M, int SEED, bool DIAGK, bool SAVE = false>
+// MF: the increment inner products of the RBF seed on the matrix cores (RbfSeedPk::mfma_pc), 4 rows
+// per batch, instead of packed VALU dots.
+template <int DP, int W, int LP, int M, int SEED, bool DIAGK, bool SAVE = false, bool MF = false>
 #ifdef GPSIG_FO_LB
 #define GPSIG_FO_BOUNDS __launch_bounds__(256, GPSIG_FO_LB)
 #else
@@ -81,10 +83,20 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
   // One row: seed cells, then the level recursion.  S_m = exclusive prefix over (rows < i, cols < j)
   // of R_m = exclusive scan over j of C_m; the M-1 scans are independent and interleave.
   using Rec = std::conditional_t<PK, typename RbfSeedPk<DP, W>::Row, RowData<DP>>;
-  auto do_row = [&](const Rec &rd, bool anch) {
+  auto do_row = [&](const Rec &rd, bool anch, const f2 *pc = nullptr) {
     f2 dM[W2];
     if constexpr (PK) {
-      seed.row(rd, anch, dM);
+      if (MF && pc) {
+        f2 pp[W2], cc[W2];
+#pragma unroll
+        for (int w2 = 0; w2 < W2; ++w2) {
+          pp[w2] = pc[w2];
+          cc[w2] = pc[W2 + w2];
+        }
+        seed.row_pc(rd, anch, pp, cc, dM);
+      } else {
+        seed.row(rd, anch, dM);
+      }
     } else {
       float d1[W];
       seed.template row<true>(rd, d1);
@@ -126,7 +138,26 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
 #define GPSIG_FO_UNROLL2 (W <= 4)
 #endif
   int i = 0;
-  if constexpr (PK && GPSIG_FO_UNROLL2) {
+  if constexpr (PK && MF) {
+    static_assert(PSeed::ANCHOR % 4 == 0, "anchor period");
+    for (; i + 4 <= nrows; i += 4) {
+      f4 P[W], Q[W];
+      seed.mfma_pc(fx, i, P, Q);
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        Rec rd;
+        rd.load(fx, i + r);
+        f2 pc[2 * W2];
+#pragma unroll
+        for (int w2 = 0; w2 < W2; ++w2) {
+          pc[w2] = (f2){P[w2][r], P[w2 + W2][r]};
+          pc[W2 + w2] = (f2){Q[w2][r], Q[w2 + W2][r]};
+        }
+        do_row(rd, r == 3 && ((i + 3) % PSeed::ANCHOR) == PSeed::ANCHOR - 1, pc);
+      }
+    }
+  }
+  if constexpr (PK && GPSIG_FO_UNROLL2 && !MF) {
     // row pairs: ANCHOR is even, so the first row of a pair never anchors (compile-time)
     static_assert(PSeed::ANCHOR % 2 == 0, "anchor period");
     for (; i + 2 <= nrows; i += 2) {
@@ -203,7 +234,12 @@ __host__ __device__ constexpr int fo_wmax(int DP, int M) {
 }
 // longest sequences: W may exceed fo_wmax at LP = 64 (register spills, still correct)
 __host__ __device__ constexpr int fo_wcap(int DP) { return DP <= 16 ? 8 : 4; }
-inline Geo fo_geometry(int l2, int DP, int M) {
+inline Geo fo_geometry(int l2, int DP, int M, bool mf = false) {
+  if (mf) {  // matrix-core seed (RBF difference seed only): W = 4 columns per lane
+    for (int LP : {16, 32, 64})
+      if (LP * 4 >= l2) return {4, LP};
+    return {0, 0};
+  }
   // smallest LP (shortest scans) at which some W <= fo_wmax covers the sequence, smallest such W
   for (int LP : {16, 32, 64})
     for (int W = 2; W <= fo_wmax(DP, M); W *= 2)
@@ -214,26 +250,36 @@ inline Geo fo_geometry(int l2, int DP, int M) {
 }
 constexpr int FO_MAX_LEVELS = 8;
 
-template <int DP, int W, int LP, int M, int SEED>
+template <int DP, int W, int LP, int M, int SEED, bool MF = false>
 int launch_fo(const SigArgs &a, long long nblocks, hipStream_t s) {
   if (nblocks <= 0) return GPSIG_OK;
   constexpr bool DIFF = SEED == SEED_RBF_DIFF || SEED == SEED_LIN_DIFF;
   if (a.pair_mode == GPSIG_PAIRS_DIAG) {
-    hipLaunchKernelGGL((sig_fo_kernel<DP, W, LP, M, SEED, true>), dim3((unsigned)nblocks), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((sig_fo_kernel<DP, W, LP, M, SEED, true, false, MF>), dim3((unsigned)nblocks), dim3(256), 0, s, a);
   } else if (a.state) {
-    if constexpr (DIFF)
+    if constexpr (DIFF && !MF)
       hipLaunchKernelGGL((sig_fo_kernel<DP, W, LP, M, SEED, false, true>), dim3((unsigned)nblocks), dim3(256), 0, s, a);
     else
       return GPSIG_EUNSUPPORTED;
   } else {
-    hipLaunchKernelGGL((sig_fo_kernel<DP, W, LP, M, SEED, false>), dim3((unsigned)nblocks), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((sig_fo_kernel<DP, W, LP, M, SEED, false, false, MF>), dim3((unsigned)nblocks), dim3(256), 0, s, a);
   }
   return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
 }
 
 template <int DP, int M, int SEED>
 int fo_geo(const SigArgs &a, long long nblocks, hipStream_t s) {
-  const Geo geo = fo_geometry(a.l2, DP, M);
+  const Geo geo = fo_geometry(a.l2, DP, M, a.mfma != 0);
+  if constexpr (SEED == SEED_RBF_DIFF) {
+    if (a.mfma) {  // A/B variant: seed dots on the matrix cores (not for the saved-state launch)
+      if (a.state) return GPSIG_EUNSUPPORTED;
+      if (geo.W == 4 && geo.LP == 16) return launch_fo<DP, 4, 16, M, SEED, true>(a, nblocks, s);
+      if (geo.W == 4 && geo.LP == 32) return launch_fo<DP, 4, 32, M, SEED, true>(a, nblocks, s);
+      if (geo.W == 4 && geo.LP == 64) return launch_fo<DP, 4, 64, M, SEED, true>(a, nblocks, s);
+      return GPSIG_EUNSUPPORTED;
+    }
+  }
+  if (a.mfma) return GPSIG_EUNSUPPORTED;
   constexpr int WM = fo_wmax(DP, M), WC = fo_wcap(DP);
 #define GPSIG_GEO(w, lp) \
   if (geo.W == w && geo.LP == lp) return launch_fo<DP, w, lp, M, SEED>(a, nblocks, s);
@@ -246,17 +292,10 @@ int fo_geo(const SigArgs &a, long long nblocks, hipStream_t s) {
   return GPSIG_EUNSUPPORTED;
 }
 
-// One explicit instantiation per (channel count, level count) lives in its own translation unit
-// (sig_fo_inst.hip compiled with -DGPSIG_DP=.. -DGPSIG_M=..), so the instantiations build in parallel.
+// sig_fo_launch_dpm<DP, M> (the per-seed dispatch) is defined only in sig_fo_inst.hip, one translation
+// unit per (channel count, level count): a definition visible here would make every includer instantiate
+// (and embed device code for) all of them.
 template <int DP, int M>
-int sig_fo_launch_dpm(const SigArgs &a, int seed, long long nblocks, hipStream_t s) {
-  switch (seed) {
-    case SEED_RBF_DIFF: return fo_geo<DP, M, SEED_RBF_DIFF>(a, nblocks, s);
-    case SEED_LIN_DIFF: return fo_geo<DP, M, SEED_LIN_DIFF>(a, nblocks, s);
-    case SEED_RBF_POINT: return fo_geo<DP, M, SEED_RBF_POINT>(a, nblocks, s);
-    case SEED_LIN_POINT: return fo_geo<DP, M, SEED_LIN_POINT>(a, nblocks, s);
-    default: return GPSIG_EUNSUPPORTED;
-  }
-}
+int sig_fo_launch_dpm(const SigArgs &a, int seed, long long nblocks, hipStream_t s);
 
 }  // namespace gpsig

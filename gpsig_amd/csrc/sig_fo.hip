@@ -79,7 +79,7 @@ static int fo_dp(const SigArgs &a, int seed, long long nblocks, hipStream_t s) {
 }
 
 int sig_fo_launch(const SigArgs &a, int DP, int seed, long long nblocks, hipStream_t s) {
-  if (fo_geometry(a.l2, DP, a.M).W == 0) return GPSIG_EUNSUPPORTED;
+  if (fo_geometry(a.l2, DP, a.M, a.mfma != 0).W == 0) return GPSIG_EUNSUPPORTED;
   switch (DP) {
 #define CASE(v) \
   case v: return fo_dp<v>(a, seed, nblocks, s);
@@ -89,6 +89,6 @@ int sig_fo_launch(const SigArgs &a, int DP, int seed, long long nblocks, hipStre
   }
 }
 
-int fo_lanes_per_pair(int l2, int DP, int M) { return fo_geometry(l2, DP, M).LP; }
+int fo_lanes_per_pair(int l2, int DP, int M, bool mf) { return fo_geometry(l2, DP, M, mf).LP; }
 
 }  // namespace gpsig

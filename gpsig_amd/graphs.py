@@ -39,11 +39,14 @@ class GraphedCall:
         self.graph = torch.cuda.CUDAGraph()
         with torch.no_grad(), torch.cuda.graph(self.graph, stream=self.stream):
             self.static_out = fn(*self.static_in)
-        # the captured launches address the per-stream scratch buffers: hold them for the graph's
-        # lifetime (gpsig_amd.ops.release_workspaces() only drops the cache's references)
+        # the captured launches address this capture stream's scratch buffer: hold it for the graph's
+        # lifetime (gpsig_amd.ops.release_workspaces() only drops the cache's references); other
+        # streams' buffers stay releasable
         from . import ops
+        key = (torch.cuda.current_device() if example_inputs[0].device.index is None
+               else example_inputs[0].device.index, self.stream.cuda_stream)
         with ops._ws_lock:
-            self._scratch = list(ops._ws.values())
+            self._scratch = ops._ws.get(key)
 
     def __call__(self, *inputs):
         if len(inputs) != len(self.static_in):

@@ -40,7 +40,12 @@ enum gpsig_status {
 /* Base (state-space) kernels, gpsig/kernels.py:966-1173. */
 enum gpsig_base_kind {
   GPSIG_BASE_RBF = 0,    /* SignatureRBF._rbf      kernels.py:1042 : exp(-|x-y|^2/2)  */
-  GPSIG_BASE_LINEAR = 1  /* SignatureLinear._lin   kernels.py:979  : <x, y>           */
+  GPSIG_BASE_LINEAR = 1, /* SignatureLinear._lin   kernels.py:979  : <x, y>           */
+  /* Flag OR-ed into base_kind of gpsig_sig_gram / gpsig_sig_diag (RBF, order 1, difference 1, no saved
+   * state): evaluate the seed's increment inner products <y_j, dx_i>, <dy_j, dx_i> (the reference's
+   * seed GEMM, kernels.py:946-957 + 1042-1044) on the matrix cores (v_mfma_f32_4x4x1_16b_f32) instead of
+   * packed VALU FMAs.  Bitwise the same results; slower on MI355X, kept as the A/B arm. */
+  GPSIG_BASE_SEED_MFMA = 0x100
 };
 
 /* Which (a, b) sequence pairs a Gram call evaluates. */

@@ -180,3 +180,28 @@ def test_unsupported_configurations_raise(case):
     X = torch.zeros((2, L, D), device=DEV)
     with pytest.raises(gpsig_amd.GpsigError):
         ops.sig_gram(X, None, M)
+
+
+@pytest.mark.parametrize("L,D,M", [(20, 3, 4), (50, 5, 5), (100, 5, 5), (128, 8, 6), (200, 2, 3)])
+def test_mfma_seed_arm_matches_valu_arm(L, D, M):
+    """The matrix-core seed (GPSIG_BASE_SEED_MFMA, v_mfma_f32_4x4x1_16b_f32 for <y_j, dx_i> and
+    <dy_j, dx_i>) is the A/B arm of the packed-VALU seed: same cells (an MFMA is a k-ordered fp32 fma
+    chain), so the Gram agrees with the VALU arm to rounding of the recursion's association and with the
+    oracle within the north_star tolerance, for the Gram, the cross Gram and the diagonal."""
+    from gpsig_amd import _lib as Lb
+    from gpsig_amd import ops
+    rng = np.random.default_rng(L + D)
+    N = 12
+    X = np.cumsum(rng.standard_normal((N, L, D)), 1) / np.sqrt(L * D)
+    Y = np.cumsum(rng.standard_normal((7, L - 3, D)), 1) / np.sqrt(L * D)
+    mf = Lb.BASE_RBF | Lb.BASE_SEED_MFMA
+    ref = kr.SignatureKernelRef(L * D, D, M, normalization=False)
+    for Yin in (None, Y):
+        a = ops.sig_gram(t(X), None if Yin is None else t(Yin), M, base=mf).cpu().numpy()
+        v = ops.sig_gram(t(X), None if Yin is None else t(Yin), M).cpu().numpy()
+        e = ref.K_seq(X, X if Yin is None else Yin)
+        assert (norm_rel_err(a[1:], v[1:], axis_levels=True) < 1e-6).all()
+        assert (norm_rel_err(a[1:], e[1:], axis_levels=True) < TOL).all()
+    dm = ops.sig_diag(t(X), M, base=mf).cpu().numpy()
+    dv = ops.sig_diag(t(X), M).cpu().numpy()
+    assert (norm_rel_err(dm[1:], dv[1:], axis_levels=True) < 1e-6).all()

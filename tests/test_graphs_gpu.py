@@ -71,9 +71,15 @@ def test_graph_survives_workspace_release():
     X0 = torch.tensor(walks(N, L, D, 7).reshape(N, -1), device=DEV, dtype=torch.float32)
     g = GraphedCall(lambda X: k.K(X), X0)
     ops.release_workspaces()
-    junk = [torch.full((1 << 20,), 7.0, device=DEV) for _ in range(8)]  # reuse of freed blocks, if any
+    # allocate on the capture stream: the caching allocator would hand these blocks out first if the
+    # graph's scratch had really been freed
+    with torch.cuda.stream(g.stream):
+        junk = [torch.full((1 << s,), 7.0, device=DEV) for s in range(12, 22) for _ in range(2)]
+    torch.cuda.current_stream().wait_stream(g.stream)
     X1 = torch.tensor(walks(N, L, D, 8).reshape(N, -1), device=DEV, dtype=torch.float32)
     got = g(X1).clone()
+    torch.cuda.synchronize()
     with torch.no_grad():
         assert torch.equal(got, k.K(X1))
+    assert all(bool((j == 7.0).all()) for j in junk)  # the replay wrote only into its own scratch
     del junk

@@ -7,6 +7,10 @@ F="--offload-arch=gfx950 -O3 -std=c++17 -fno-slp-vectorize"
 b() { name=$1; shift; hipcc $F -DVARIANT=\"$name\" "$@" tools/kbench.hip -o tools/bin/$name & }
 b g_w4 -DKW=4 -DKLP=32
 b g_w8 -DKW=8 -DKLP=16
-b g_w8_nn -DKW=8 -DKLP=16 -DGPSIG_NAIVE=0
+# MFMA seed (RbfSeedPk::mfma_pc) A/B
+b g_w4_mf -DKW=4 -DKLP=32 -DKMF=1
+b g_w4_mf_lb3 -DKW=4 -DKLP=32 -DKMF=1 -DGPSIG_FO_LB=3
+b g_w8_mf -DKW=8 -DKLP=16 -DKMF=1
+b g_w8_mf_lb2 -DKW=8 -DKLP=16 -DKMF=1 -DGPSIG_FO_LB=2
 wait
 ls tools/bin

@@ -26,6 +26,9 @@
 #ifndef KLP
 #define KLP 32
 #endif
+#ifndef KMF
+#define KMF 0
+#endif
 
 using namespace gpsig;
 
@@ -102,7 +105,7 @@ int main(int argc, char **argv) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   auto launch = [&]() {
-    hipLaunchKernelGGL((sig_fo_kernel<DP, KW, KLP, KM, SEED_RBF_DIFF, false>),
+    hipLaunchKernelGGL((sig_fo_kernel<DP, KW, KLP, KM, SEED_RBF_DIFF, false, false, (KMF != 0)>),
                        dim3((unsigned)nblocks), dim3(256), 0, 0, p);
   };
   launch();
@@ -113,9 +116,16 @@ int main(int argc, char **argv) {
   CK(hipEventSynchronize(e1));
   float ms;
   CK(hipEventElapsedTime(&ms, e0, e1));
-  std::vector<float> out(64);
-  CK(hipMemcpy(out.data(), dOut, 64 * 4, hipMemcpyDeviceToHost));
-  printf("%s n=%d L=%d D=%d M=%d ms=%.3f entries/s=%.4g chk=%.6f\n", VARIANT, n, l, d, M, ms / reps,
-         (double)n * n / (ms / reps / 1e3), out[1]);
+  // checksum of the upper triangle (the launch stores both triangles; compare variants by it)
+  std::vector<float> out((size_t)n * n);
+  CK(hipMemcpy(out.data(), dOut, out.size() * 4, hipMemcpyDeviceToHost));
+  double cs = 0, ca = 0;
+  for (int a = 0; a < n; ++a)
+    for (int b = a; b < n; ++b) {
+      cs += out[(size_t)a * n + b] * (1.0 + 1e-3 * ((a * 7 + b) % 13));
+      ca += std::fabs(out[(size_t)a * n + b]);
+    }
+  printf("%s n=%d L=%d D=%d M=%d ms=%.3f entries/s=%.4g chk=%.9e abs=%.9e\n", VARIANT, n, l, d, M, ms / reps,
+         (double)n * n / (ms / reps / 1e3), cs, ca);
   return 0;
 }
