@@ -36,6 +36,7 @@ struct SigArgs {
   long long out_ld, out_lvl;  // row stride, level stride (elements)
   float *state;               // optional saved forward state for the VJP (gpsig_sig_gram_state)
   int mfma;                   // RBF difference seed: increment dots on the matrix cores (GPSIG_BASE_SEED_MFMA)
+  int nblk;                   // column blocks per pair (first order, LP = 64; 1 = unblocked)
 };
 
 // Saved forward state of a first-order pair (gpsig_sig_gram_state): column sums of levels 1..M-1
@@ -183,7 +184,7 @@ struct RowSeed {
         float c = 0.0f;
 #pragma unroll
         for (int k = 0; k < DP; ++k) c = __builtin_fmaf(rd.dx[k], dy[w][k], c);
-        dM[w] = c;  // padded columns have dy == 0
+        dM[w] = (w + 1 < W || valid_last) ? c : 0.0f;  // padded columns have dy == 0; the halo cell of a block is masked
       }
     } else if constexpr (SEED == SEED_RBF_POINT) {
 #pragma unroll
@@ -243,7 +244,8 @@ struct RbfSeedPk {
   GPSIG_DEV void init(const float *__restrict__ fx, const float *__restrict__ fy, int gl, int l2) {
     const int ncols = l2 - 1;
     // columns past the sequence clamp to its last point (zero increment): their cells are exact
-    // zeros in the product form; only the lane's last column can see a foreign right neighbour
+    // zeros in the product form; only the lane's last column can see a foreign right neighbour.
+    // l2 = points of this column block (its last one the halo point when the block is not the last)
 #pragma unroll
     for (int w2 = 0; w2 < W2; ++w2)
 #pragma unroll
@@ -251,12 +253,15 @@ struct RbfSeedPk {
         const int j = gl * W + w2 + h * W2;  // pair w2 = columns (w2, w2 + W/2) of the lane
         const int jj = j < l2 ? j : l2 - 1;
         const float *f = fy + (long long)jj * FS;
+        // a column with no cell (past the sequence, or the right halo point of a column block) gets a
+        // zero increment, so its product-form cell is exactly 0
+        const bool cell = j < ncols;
 #pragma unroll
         for (int k = 0; k < DP; ++k) {
           y[w2][k][h] = f[k];
-          dy[w2][k][h] = f[DP + k];
+          dy[w2][k][h] = cell ? f[DP + k] : 0.0f;
         }
-        hdy[w2][h] = f[2 * DP];
+        hdy[w2][h] = cell ? f[2 * DP] : 0.0f;
         if (w2 == W2 - 1 && h == 1) valid_last = j < ncols;
       }
     float x0[DP];

@@ -70,145 +70,183 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
   constexpr bool PK = (SEED == SEED_RBF_DIFF);
   using PSeed = std::conditional_t<PK, RbfSeedPk<DP, W>, RowSeed<DP, W, SEED>>;
   constexpr int W2 = W / 2;
-  PSeed seed;
-  seed.init(fx, fy, gl, p.l2);
-
-  f2 C[M][W2];
-#pragma unroll
-  for (int m = 0; m < M; ++m)
-#pragma unroll
-    for (int w2 = 0; w2 < W2; ++w2) C[m][w2] = splat2(0.0f);
-
+  constexpr int ML = M > 1 ? M - 1 : 1;
   const int nrows = Seed::DIFF ? p.l1 - 1 : p.l1;
-  // One row: seed cells, then the level recursion.  S_m = exclusive prefix over (rows < i, cols < j)
-  // of R_m = exclusive scan over j of C_m; the M-1 scans are independent and interleave.
-  using Rec = std::conditional_t<PK, typename RbfSeedPk<DP, W>::Row, RowData<DP>>;
-  auto do_row = [&](const Rec &rd, bool anch, const f2 *pc = nullptr) {
-    f2 dM[W2];
-    if constexpr (PK) {
-      if (MF && pc) {
-        f2 pp[W2], cc[W2];
+
+  // Column blocks (sequences longer than one lane group covers, LP = 64 only): block k holds the
+  // cells j0 .. j0 + CPB - 1 (j0 = k CPB) on the points j0 .. j0 + CPB (the last lane's last column is
+  // the block's right halo point, its cell is masked), streamed over all rows before the next block.
+  // The exclusive column prefix of block k adds the carry c_m(i) = sum_{j < j0} C_m(i, j) of the blocks
+  // to its left, one float per row and level kept in this wave's LDS slab (written by block k-1,
+  // read and advanced by block k).
+  constexpr int CPB = LP * W - 1;
+  const int nblk = (LP == 64) ? p.nblk : 1;
+  extern __shared__ float fo_carry[];
+  float *__restrict__ carry = fo_carry + (long long)wave * nrows * ML;
+
+  float Kacc[M];
 #pragma unroll
-        for (int w2 = 0; w2 < W2; ++w2) {
-          pp[w2] = pc[w2];
-          cc[w2] = pc[W2 + w2];
+  for (int m = 0; m < M; ++m) Kacc[m] = 0.0f;
+
+  for (int blk = 0; blk < nblk; ++blk) {
+    const int j0 = blk * CPB;
+    // points of this block: the DIFF seeds see the halo point, the point seeds do not
+    const int npts = nblk == 1 ? p.l2 : min(p.l2 - j0, Seed::DIFF ? CPB + 1 : CPB);
+    PSeed seed;
+    seed.init(fx, fy + (long long)j0 * FS, gl, npts);
+
+    f2 C[M][W2];
+#pragma unroll
+    for (int m = 0; m < M; ++m)
+#pragma unroll
+      for (int w2 = 0; w2 < W2; ++w2) C[m][w2] = splat2(0.0f);
+
+    // One row: seed cells, then the level recursion.  S_m = exclusive prefix over (rows < i, cols < j)
+    // of R_m = exclusive scan over j of C_m; the M-1 scans are independent and interleave.
+    using Rec = std::conditional_t<PK, typename RbfSeedPk<DP, W>::Row, RowData<DP>>;
+    auto do_row = [&](int i, const Rec &rd, bool anch, const f2 *pc = nullptr) {
+      f2 dM[W2];
+      if constexpr (PK) {
+        if (MF && pc) {
+          f2 pp[W2], cc[W2];
+#pragma unroll
+          for (int w2 = 0; w2 < W2; ++w2) {
+            pp[w2] = pc[w2];
+            cc[w2] = pc[W2 + w2];
+          }
+          seed.row_pc(rd, anch, pp, cc, dM);
+        } else {
+          seed.row(rd, anch, dM);
         }
-        seed.row_pc(rd, anch, pp, cc, dM);
       } else {
-        seed.row(rd, anch, dM);
+        float d1[W];
+        seed.template row<true>(rd, d1);
+#pragma unroll
+        for (int w2 = 0; w2 < W2; ++w2) dM[w2] = (f2){d1[w2], d1[w2 + W2]};
       }
-    } else {
-      float d1[W];
-      seed.template row<true>(rd, d1);
+      // Column pair k of a lane holds columns (k, k + W/2), so the in-lane exclusive prefix runs on both
+      // halves at once: E_k = P_0 + ... + P_{k-1} (packed), E_{W/2} = (H_lo, H_hi) the half totals, and
+      // S_m(column) = E_k + (b, b + H_lo) with b the exclusive cross-lane prefix of T = H_lo + H_hi.
+      // The lane totals of the M-1 levels are scanned across the group together.
+      f2 E[ML][W2 + 1];
+      float T[ML], base[ML];
 #pragma unroll
-      for (int w2 = 0; w2 < W2; ++w2) dM[w2] = (f2){d1[w2], d1[w2 + W2]};
-    }
-    // Column pair k of a lane holds columns (k, k + W/2), so the in-lane exclusive prefix runs on both
-    // halves at once: E_k = P_0 + ... + P_{k-1} (packed), E_{W/2} = (H_lo, H_hi) the half totals, and
-    // S_m(column) = E_k + (b, b + H_lo) with b the exclusive cross-lane prefix of T = H_lo + H_hi.
-    // The lane totals of the M-1 levels are scanned across the group together.
-    constexpr int ML = M > 1 ? M - 1 : 1;
-    f2 E[ML][W2 + 1];
-    float T[ML], base[ML];
+      for (int m = 0; m + 1 < M; ++m) {
+        E[m][1] = C[m][0];
 #pragma unroll
-    for (int m = 0; m + 1 < M; ++m) {
-      E[m][1] = C[m][0];
+        for (int k = 2; k <= W2; ++k) E[m][k] = E[m][k - 1] + C[m][k - 1];
+        T[m] = E[m][W2][0] + E[m][W2][1];
+        base[m] = T[m];
+      }
+      if constexpr (M > 1) group_incl_scan_n<LP, ML>(base);
+      if constexpr (LP == 64 && M > 1) {
+        if (nblk > 1) {  // wave-uniform: carry in from the blocks to the left, carry out to the right
+          float *__restrict__ cr = carry + (long long)i * ML;
 #pragma unroll
-      for (int k = 2; k <= W2; ++k) E[m][k] = E[m][k - 1] + C[m][k - 1];
-      T[m] = E[m][W2][0] + E[m][W2][1];
-      base[m] = T[m];
-    }
-    if constexpr (M > 1) group_incl_scan_n<LP, ML>(base);
-    // descending m: level m reads C_m (through E) before level m-1's update writes it
+          for (int m = 0; m < ML; ++m) {
+            const float cin = blk > 0 ? cr[m] : 0.0f;
+            const float tot = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, base[m]), 63));
+            if (blk + 1 < nblk && lane == 0) cr[m] = cin + tot;
+            base[m] += cin;
+          }
+        }
+      }
+      // descending m: level m reads C_m (through E) before level m-1's update writes it
 #pragma unroll
-    for (int m = M - 2; m >= 0; --m) {
-      f2 off;
-      off[0] = base[m] - T[m];
-      off[1] = off[0] + E[m][W2][0];
-      C[m + 1][0] = fma2(dM[0], off, C[m + 1][0]);
+      for (int m = M - 2; m >= 0; --m) {
+        f2 off;
+        off[0] = base[m] - T[m];
+        off[1] = off[0] + E[m][W2][0];
+        C[m + 1][0] = fma2(dM[0], off, C[m + 1][0]);
 #pragma unroll
-      for (int k = 1; k < W2; ++k) C[m + 1][k] = fma2(dM[k], E[m][k] + off, C[m + 1][k]);
-    }
+        for (int k = 1; k < W2; ++k) C[m + 1][k] = fma2(dM[k], E[m][k] + off, C[m + 1][k]);
+      }
 #pragma unroll
-    for (int w2 = 0; w2 < W2; ++w2) C[0][w2] += dM[w2];
-  };
-  // Row loop.  For the packed RBF seed the row recurrences are re-anchored every ANCHOR rows (a
-  // wave-uniform branch); the other seeds evaluate every row directly.
+      for (int w2 = 0; w2 < W2; ++w2) C[0][w2] += dM[w2];
+    };
+    // Row loop.  For the packed RBF seed the row recurrences are re-anchored every ANCHOR rows (a
+    // wave-uniform branch); the other seeds evaluate every row directly.
 #ifndef GPSIG_FO_UNROLL2
 #define GPSIG_FO_UNROLL2 (W <= 4)
 #endif
-  int i = 0;
-  if constexpr (PK && MF) {
-    static_assert(PSeed::ANCHOR % 4 == 0, "anchor period");
-    for (; i + 4 <= nrows; i += 4) {
-      f4 P[W], Q[W];
-      seed.mfma_pc(fx, i, P, Q);
+    int i = 0;
+    if constexpr (PK && MF) {
+      static_assert(PSeed::ANCHOR % 4 == 0, "anchor period");
+      for (; i + 4 <= nrows; i += 4) {
+        f4 P[W], Q[W];
+        seed.mfma_pc(fx, i, P, Q);
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        Rec rd;
-        rd.load(fx, i + r);
-        f2 pc[2 * W2];
+        for (int r = 0; r < 4; ++r) {
+          Rec rd;
+          rd.load(fx, i + r);
+          f2 pc[2 * W2];
 #pragma unroll
-        for (int w2 = 0; w2 < W2; ++w2) {
-          pc[w2] = (f2){P[w2][r], P[w2 + W2][r]};
-          pc[W2 + w2] = (f2){Q[w2][r], Q[w2 + W2][r]};
+          for (int w2 = 0; w2 < W2; ++w2) {
+            pc[w2] = (f2){P[w2][r], P[w2 + W2][r]};
+            pc[W2 + w2] = (f2){Q[w2][r], Q[w2 + W2][r]};
+          }
+          do_row(i + r, rd, r == 3 && ((i + 3) % PSeed::ANCHOR) == PSeed::ANCHOR - 1, pc);
         }
-        do_row(rd, r == 3 && ((i + 3) % PSeed::ANCHOR) == PSeed::ANCHOR - 1, pc);
       }
     }
-  }
-  if constexpr (PK && GPSIG_FO_UNROLL2 && !MF) {
-    // row pairs: ANCHOR is even, so the first row of a pair never anchors (compile-time)
-    static_assert(PSeed::ANCHOR % 2 == 0, "anchor period");
-    for (; i + 2 <= nrows; i += 2) {
-      Rec r0, r1;
-      r0.load(fx, i);
-      r1.load(fx, i + 1);
-      do_row(r0, false);
-      do_row(r1, ((i + 1) % PSeed::ANCHOR) == PSeed::ANCHOR - 1);
+    if constexpr (PK && GPSIG_FO_UNROLL2 && !MF) {
+      // row pairs: ANCHOR is even, so the first row of a pair never anchors (compile-time)
+      static_assert(PSeed::ANCHOR % 2 == 0, "anchor period");
+      for (; i + 2 <= nrows; i += 2) {
+        Rec r0, r1;
+        r0.load(fx, i);
+        r1.load(fx, i + 1);
+        do_row(i, r0, false);
+        do_row(i + 1, r1, ((i + 1) % PSeed::ANCHOR) == PSeed::ANCHOR - 1);
+      }
     }
-  }
-  for (; i < nrows; ++i) {
-    Rec rd;
-    bool anch = true;
-    if constexpr (PK) {
-      rd.load(fx, i);
-      anch = (i % PSeed::ANCHOR) == PSeed::ANCHOR - 1;
-    } else {
-      rd.load(fx, i, SEED);
+    for (; i < nrows; ++i) {
+      Rec rd;
+      bool anch = true;
+      if constexpr (PK) {
+        rd.load(fx, i);
+        anch = (i % PSeed::ANCHOR) == PSeed::ANCHOR - 1;
+      } else {
+        rd.load(fx, i, SEED);
+      }
+      do_row(i, rd, anch);
     }
-    do_row(rd, anch);
+
+    // ---- saved VJP state (gpsig_sig_gram_state): column sums of levels 1..M-1 (column pair k holds
+    // columns k, k + W/2), before the epilogue so it adds no live registers there
+    static_assert(!SAVE || (!DIAGK && Seed::DIFF), "saved state: Gram pairs of a DIFF seed");
+    if constexpr (SAVE) {
+      if (pair_ok) {
+        const int nc = p.l2 - 1;
+        float *__restrict__ st = p.state + state_slot(a, b, p.n2, p.pair_mode == GPSIG_PAIRS_UPPER) * state_stride(M, p.l2);
+#pragma unroll
+        for (int m = 0; m + 1 < M; ++m)
+#pragma unroll
+          for (int w2 = 0; w2 < W2; ++w2)
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+              const int jl = gl * W + w2 + h * W2;
+              const int j = j0 + jl;
+              if (j < nc && jl < CPB) st[(long long)m * nc + j] = C[m][w2][h];
+            }
+      }
+    }
+
+    // ---- this block's share of K_m = sum_j C_m(j)
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      f2 s2 = C[m][0];
+#pragma unroll
+      for (int w2 = 1; w2 < W2; ++w2) s2 += C[m][w2];
+      Kacc[m] += group_sum<LP>(s2[0] + s2[1]);
+    }
   }
 
-  // ---- saved VJP state (gpsig_sig_gram_state): column sums of levels 1..M-1 (column pair k holds
-  // columns k, k + W/2), before the epilogue so it adds no live registers there
-  static_assert(!SAVE || (!DIAGK && Seed::DIFF), "saved state: Gram pairs of a DIFF seed");
-  if constexpr (SAVE) {
-    if (pair_ok) {
-      const int nc = p.l2 - 1;
-      float *__restrict__ st = p.state + state_slot(a, b, p.n2, p.pair_mode == GPSIG_PAIRS_UPPER) * state_stride(M, p.l2);
-#pragma unroll
-      for (int m = 0; m + 1 < M; ++m)
-#pragma unroll
-        for (int w2 = 0; w2 < W2; ++w2)
-#pragma unroll
-          for (int h = 0; h < 2; ++h) {
-            const int j = gl * W + w2 + h * W2;
-            if (j < nc) st[(long long)m * nc + j] = C[m][w2][h];
-          }
-    }
-  }
-
-  // ---- epilogue: K_m = sum_j C_m(j)
+  // ---- epilogue
   float K[M + 1];
   K[0] = 1.0f;
 #pragma unroll
-  for (int m = 0; m < M; ++m) {
-    f2 s2 = C[m][0];
-#pragma unroll
-    for (int w2 = 1; w2 < W2; ++w2) s2 += C[m][w2];
-    K[m + 1] = group_sum<LP>(s2[0] + s2[1]);
-  }
+  for (int m = 0; m < M; ++m) K[m + 1] = Kacc[m];
   if (gl == 0 && pair_ok) {
     if constexpr (Seed::DIFF) K[1] = level1_closed<DP, SEED>(fx, fy, p.l1, p.l2);
     store_pair<M>(p, a, b, K);
@@ -232,10 +270,10 @@ struct Geo { int W, LP; };
 __host__ __device__ constexpr int fo_wmax(int DP, int M) {
   return DP <= 5 ? 8 : (DP <= 6 ? (M <= 5 ? 8 : 4) : (DP <= 16 ? 4 : 2));
 }
-// longest sequences: W may exceed fo_wmax at LP = 64 (register spills, still correct)
-__host__ __device__ constexpr int fo_wcap(int DP) { return DP <= 16 ? 8 : 4; }
+// Sequences longer than 64 * fo_wmax points run at LP = 64, W = fo_wmax in column blocks
+// (sig_fo_kernel, `nblk`), with one float per row and level of carry in LDS per wave.
 inline Geo fo_geometry(int l2, int DP, int M, bool mf = false) {
-  if (mf) {  // matrix-core seed (RBF difference seed only): W = 4 columns per lane
+  if (mf) {  // matrix-core seed (RBF difference seed only): W = 4 columns per lane, no column blocks
     for (int LP : {16, 32, 64})
       if (LP * 4 >= l2) return {4, LP};
     return {0, 0};
@@ -244,25 +282,37 @@ inline Geo fo_geometry(int l2, int DP, int M, bool mf = false) {
   for (int LP : {16, 32, 64})
     for (int W = 2; W <= fo_wmax(DP, M); W *= 2)
       if (LP * W >= l2) return {W, LP};
-  for (int W = 2 * fo_wmax(DP, M); W <= fo_wcap(DP); W *= 2)
-    if (64 * W >= l2) return {W, 64};
-  return {0, 0};
+  return {fo_wmax(DP, M), 64};
 }
+// Column blocks of a launch: cells per block LP*W - 1 (the last column of the last lane is the halo point)
+inline int fo_blocks(int l2, bool diff, Geo g) {
+  if (g.LP * g.W >= l2) return 1;
+  const int cells = diff ? l2 - 1 : l2, cpb = g.LP * g.W - 1;
+  return (cells + cpb - 1) / cpb;
+}
+// LDS bytes per 4-wave workgroup for the carries of a blocked launch (0 when unblocked)
+inline size_t fo_carry_bytes(int l1, bool diff, int M, int nblk) {
+  if (nblk <= 1 || M <= 1) return 0;
+  return (size_t)4 * (diff ? l1 - 1 : l1) * (M - 1) * sizeof(float);
+}
+constexpr size_t FO_MAX_CARRY_BYTES = 160 * 1024;
 constexpr int FO_MAX_LEVELS = 8;
 
 template <int DP, int W, int LP, int M, int SEED, bool MF = false>
 int launch_fo(const SigArgs &a, long long nblocks, hipStream_t s) {
   if (nblocks <= 0) return GPSIG_OK;
   constexpr bool DIFF = SEED == SEED_RBF_DIFF || SEED == SEED_LIN_DIFF;
+  const size_t lds = LP == 64 ? fo_carry_bytes(a.l1, DIFF, M, a.nblk) : 0;
+  if (lds > FO_MAX_CARRY_BYTES) return GPSIG_EUNSUPPORTED;
   if (a.pair_mode == GPSIG_PAIRS_DIAG) {
-    hipLaunchKernelGGL((sig_fo_kernel<DP, W, LP, M, SEED, true, false, MF>), dim3((unsigned)nblocks), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((sig_fo_kernel<DP, W, LP, M, SEED, true, false, MF>), dim3((unsigned)nblocks), dim3(256), lds, s, a);
   } else if (a.state) {
     if constexpr (DIFF && !MF)
-      hipLaunchKernelGGL((sig_fo_kernel<DP, W, LP, M, SEED, false, true>), dim3((unsigned)nblocks), dim3(256), 0, s, a);
+      hipLaunchKernelGGL((sig_fo_kernel<DP, W, LP, M, SEED, false, true>), dim3((unsigned)nblocks), dim3(256), lds, s, a);
     else
       return GPSIG_EUNSUPPORTED;
   } else {
-    hipLaunchKernelGGL((sig_fo_kernel<DP, W, LP, M, SEED, false, false, MF>), dim3((unsigned)nblocks), dim3(256), 0, s, a);
+    hipLaunchKernelGGL((sig_fo_kernel<DP, W, LP, M, SEED, false, false, MF>), dim3((unsigned)nblocks), dim3(256), lds, s, a);
   }
   return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
 }
@@ -280,14 +330,12 @@ int fo_geo(const SigArgs &a, long long nblocks, hipStream_t s) {
     }
   }
   if (a.mfma) return GPSIG_EUNSUPPORTED;
-  constexpr int WM = fo_wmax(DP, M), WC = fo_wcap(DP);
+  constexpr int WM = fo_wmax(DP, M);
 #define GPSIG_GEO(w, lp) \
   if (geo.W == w && geo.LP == lp) return launch_fo<DP, w, lp, M, SEED>(a, nblocks, s);
   GPSIG_GEO(2, 16) GPSIG_GEO(2, 32) GPSIG_GEO(2, 64)
-  if constexpr (WM >= 4) { GPSIG_GEO(4, 16) GPSIG_GEO(4, 32) }
-  if constexpr (WC >= 4) { GPSIG_GEO(4, 64) }
-  if constexpr (WM >= 8) { GPSIG_GEO(8, 16) GPSIG_GEO(8, 32) }
-  if constexpr (WC >= 8) { GPSIG_GEO(8, 64) }
+  if constexpr (WM >= 4) { GPSIG_GEO(4, 16) GPSIG_GEO(4, 32) GPSIG_GEO(4, 64) }
+  if constexpr (WM >= 8) { GPSIG_GEO(8, 16) GPSIG_GEO(8, 32) GPSIG_GEO(8, 64) }
 #undef GPSIG_GEO
   return GPSIG_EUNSUPPORTED;
 }

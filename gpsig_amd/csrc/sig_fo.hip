@@ -78,8 +78,11 @@ static int fo_dp(const SigArgs &a, int seed, long long nblocks, hipStream_t s) {
   }
 }
 
-int sig_fo_launch(const SigArgs &a, int DP, int seed, long long nblocks, hipStream_t s) {
-  if (fo_geometry(a.l2, DP, a.M, a.mfma != 0).W == 0) return GPSIG_EUNSUPPORTED;
+int sig_fo_launch(const SigArgs &a0, int DP, int seed, long long nblocks, hipStream_t s) {
+  const Geo g = fo_geometry(a0.l2, DP, a0.M, a0.mfma != 0);
+  if (g.W == 0) return GPSIG_EUNSUPPORTED;
+  SigArgs a = a0;
+  a.nblk = fo_blocks(a0.l2, seed == SEED_RBF_DIFF || seed == SEED_LIN_DIFF, g);
   switch (DP) {
 #define CASE(v) \
   case v: return fo_dp<v>(a, seed, nblocks, s);

@@ -1,0 +1,87 @@
+"""GPU parity for long sequences: the first-order Gram in column blocks (sig_fo_kernel `nblk`, LP = 64,
+carries in LDS) beyond the 64 * fo_wmax points one lane group covers -- the reference's cython/TF
+paths have no length cap (signature_algs.py:8-35 over any L).  Checked against the float64 oracle
+(oracle/kernels_ref.py) at sizes it finishes in seconds, and for consistency across the block
+boundary: a pair of sequences and their truncation at a block edge agree with the unblocked kernel."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import norm_rel_err
+from oracle import kernels_ref as kr
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-5
+DEV = "cuda"
+
+
+def t(x):
+    return torch.as_tensor(np.asarray(x), device=DEV)
+
+
+def walks(n, l, d, seed):
+    rng = np.random.default_rng(seed)
+    return np.cumsum(rng.standard_normal((n, l, d)), 1) / np.sqrt(l * d)
+
+
+@pytest.mark.parametrize("L,D,M,base,diff", [
+    (600, 3, 4, "rbf", True),      # 2 blocks at W = 8 (511 cells per block)
+    (1100, 2, 3, "rbf", True),     # 3 blocks
+    (600, 8, 6, "rbf", True),      # W = 4: 255 cells per block, 3 blocks
+    (520, 4, 5, "linear", True),
+    (600, 3, 4, "rbf", False),     # point seeds (difference=False)
+    (513, 5, 2, "linear", False),
+])
+def test_long_sequences_match_oracle(L, D, M, base, diff):
+    from gpsig_amd import ops
+    X = walks(5, L, D, L + D)
+    Y = walks(3, L - 37, D, L + D + 1)
+    ref = kr.SignatureKernelRef(L * D, D, M, normalization=False, base=base, difference=diff)
+    got = ops.sig_gram(t(X), None, M, base=base, difference=diff).cpu().numpy()
+    exp = ref.K_seq(X, X)
+    assert (norm_rel_err(got[1:], exp[1:], axis_levels=True) < TOL).all()
+    got = ops.sig_gram(t(X), t(Y), M, base=base, difference=diff).cpu().numpy()
+    exp = ref.K_seq(X, Y)
+    assert (norm_rel_err(got[1:], exp[1:], axis_levels=True) < TOL).all()
+    d = ops.sig_diag(t(X), M, base=base, difference=diff).cpu().numpy()
+    assert (norm_rel_err(d[1:], np.stack([np.diagonal(e) for e in ref.K_seq(X, X)])[1:], axis_levels=True) < TOL).all()
+
+
+def test_long_normalised_K_and_saved_state_gradient_path():
+    """SignatureRBF.K at L = 700 (normalised, fused epilogue) vs the oracle; the training forward (saved
+    VJP state, gpsig_sig_gram_state) at the same length writes the same Gram."""
+    import gpsig_amd
+    from gpsig_amd import _lib as Lb
+    from gpsig_amd import ops
+    N, L, D, M = 6, 700, 3, 4
+    X = walks(N, L, D, 3)
+    k = gpsig_amd.SignatureRBF(L * D, D, M)
+    got = k.K(t(X.reshape(N, -1))).cpu().numpy()
+    exp = kr.SignatureKernelRef(L * D, D, M).K(X.reshape(N, -1))
+    assert norm_rel_err(got, exp) < TOL
+    Xd = t(X).float()
+    st = torch.zeros(ops.sig_state_numel(N, None, L, M), dtype=torch.float32, device=DEV)
+    a = ops.sig_gram(Xd, None, M, state=st).cpu().numpy()
+    b = ops.sig_gram(Xd, None, M).cpu().numpy()
+    np.testing.assert_array_equal(a, b)
+    assert torch.isfinite(st).all()
+
+
+def test_block_boundary_consistency():
+    """Cells on either side of a block edge: the Gram of sequences of exactly 512 points (one block of
+    511 cells at W = 8, LP = 64) and of 513 points (two blocks, the second holding one cell) both match
+    the oracle -- the halo point and carry are exact at the seam."""
+    from gpsig_amd import ops
+    for L in (512, 513, 1023, 1024):
+        X = walks(4, L, 3, L)
+        ref = kr.SignatureKernelRef(L * 3, 3, 5, normalization=False)
+        got = ops.sig_gram(t(X), None, 5).cpu().numpy()
+        assert (norm_rel_err(got[1:], ref.K_seq(X, X)[1:], axis_levels=True) < TOL).all(), L
+
+
+def test_carry_too_large_raises():
+    from gpsig_amd import _lib as Lb
+    from gpsig_amd import ops
+    X = torch.zeros((2, 6000, 2), device=DEV)  # 4 waves x 5999 rows x 7 levels x 4 B > 160 KiB of LDS
+    with pytest.raises(Lb.GpsigError):
+        ops.sig_gram(X, None, 8)
