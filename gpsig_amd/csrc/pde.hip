@@ -153,10 +153,17 @@ __global__ __launch_bounds__(256) void pde_kernel(PdeArgs p) {
 // evaluates the lane's W/REP coarse increments and update coefficients once and then sweeps REP fine
 // rows x W fine columns; the skew is one step per coarse row, the left boundary of the REP rows comes
 // from lane l-1 (REP DPP moves per step).
+//
+// Column blocks (more than 64 W fine columns): the wave sweeps the grid in blocks of 64 W columns,
+// left to right.  The last lane of a block hands its right column K[i][c0 + 64 W - 1] (all rows i) to
+// the next block through this wave's LDS slab `bnd` (I + 1 doubles), where lane 0 reads it as its left
+// boundary; lane 0 reads row i at step i and the last lane overwrites it at step i + 63, so one slab
+// serves every block in place.
 template <typename T, int DP, int W, int REP, int SOLVER>
 __global__ __launch_bounds__(256) void pde_rep_kernel(PdeArgs p) {
   static_assert(W % REP == 0, "a lane owns whole coarse columns");
   constexpr int WC = W / REP;
+  constexpr int CB = 64 * W;  // fine columns per block
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int lane = threadIdx.x & 63;
   const int wave = wave_uniform(threadIdx.x >> 6);
@@ -185,7 +192,8 @@ __global__ __launch_bounds__(256) void pde_rep_kernel(PdeArgs p) {
 
   const T inv_factor = (T)1.0 / (T)(REP * REP);
   const int IC = p.l1 - 1, JC = p.l2 - 1;  // coarse rows / columns
-  const int J = REP * JC;
+  const int I = REP * IC, J = REP * JC;
+  const int nblk = (J + CB - 1) / CB;
   const int d = p.d;
   const float *x = p.X + (long long)a * p.l1 * d;
   const float *y = p.Y + (long long)b * p.l2 * d;
@@ -194,91 +202,100 @@ __global__ __launch_bounds__(256) void pde_rep_kernel(PdeArgs p) {
   for (int r = lane; r < IC; r += 64)
 #pragma unroll
     for (int k = 0; k < DP; ++k) dxs[r * DP + k] = k < d ? x[(r + 1) * d + k] - x[r * d + k] : 0.0f;
-
-  // y increments of this lane's coarse columns
-  float dy[WC][DP];
-#pragma unroll
-  for (int w = 0; w < WC; ++w) {
-    int cj = lane * WC + w;
-    cj = cj < JC - 1 ? cj : JC - 1;
-#pragma unroll
-    for (int k = 0; k < DP; ++k) dy[w][k] = k < d ? y[(cj + 1) * d + k] - y[cj * d + k] : 0.0f;
-  }
+  T *bnd = reinterpret_cast<T *>(lds + (((size_t)4 * IC * DP + 3) & ~(size_t)3)) + (size_t)wave * (I + 1);
   __syncthreads();
   if (!ok) return;
 
   const bool hybrid = (p.pair_mode == GPSIG_PAIRS_DIAG) && SOLVER == 0;
   constexpr bool s1 = SOLVER == 1;
   T up[W];
+  for (int blk = 0; blk < nblk; ++blk) {
+    const int c0 = blk * CB;  // first fine column of the block (a multiple of REP)
+    const bool from_left = blk > 0, to_right = blk + 1 < nblk;
+    // y increments of this lane's coarse columns
+    float dy[WC][DP];
 #pragma unroll
-  for (int w = 0; w < W; ++w) up[w] = (T)1;
-  T last[REP];  // K[row][lane*W + W - 1] of this lane's REP rows of the previous step
+    for (int w = 0; w < WC; ++w) {
+      int cj = c0 / REP + lane * WC + w;
+      cj = cj < JC - 1 ? cj : JC - 1;
 #pragma unroll
-  for (int r = 0; r < REP; ++r) last[r] = (T)1;
-  T corner_prev = (T)1;  // left boundary of the previous step's last row
-  const int lanes_used = (J + W - 1) / W;
-  const int nsteps = IC + lanes_used - 1;
-  for (int s = 0; s < nsteps; ++s) {
-    T left[REP];
-#pragma unroll
-    for (int r = 0; r < REP; ++r) {
-      left[r] = lane_prev(last[r]);
-      if (lane == 0) left[r] = (T)1;
+      for (int k = 0; k < DP; ++k) dy[w][k] = k < d ? y[(cj + 1) * d + k] - y[cj * d + k] : 0.0f;
     }
-    const int ci = s - lane;
-    if (ci >= 0 && ci < IC && lane < lanes_used) {
-      const float *dxr = dxs + ci * DP;
-      float dxv[DP];
 #pragma unroll
-      for (int k = 0; k < DP; ++k) dxv[k] = dxr[k];
-      // coefficients of the lane's coarse cells: solver 1 uses (A, B), solver 0 uses inc - 1 (as B)
-      T A[WC], B[WC];
+    for (int w = 0; w < W; ++w) up[w] = (T)1;
+    T last[REP];  // K[row][c0 + lane*W + W - 1] of this lane's REP rows of the previous step
 #pragma unroll
-      for (int w = 0; w < WC; ++w) {
-        float incf = 0.0f;
-#pragma unroll
-        for (int k = 0; k < DP; ++k) incf = __builtin_fmaf(dxv[k], dy[w][k], incf);
-        const T inc = (T)incf * inv_factor;
-        const T inc2 = inc * inc;
-        if constexpr (s1) {
-          A[w] = (T)1 + (T)0.5 * inc + (T)(1.0 / 12) * inc2;
-          B[w] = (T)1 - (T)(1.0 / 12) * inc2;
-        } else {
-          A[w] = inc;  // hybrid diagonal cells need inc
-          B[w] = inc - (T)1;
-        }
-      }
+    for (int r = 0; r < REP; ++r) last[r] = (T)1;
+    T corner_prev = (T)1;  // left boundary of the previous step's last row
+    const int lanes_used = min(64, (J - c0 + W - 1) / W);
+    const int nsteps = IC + lanes_used - 1;
+    for (int s = 0; s < nsteps; ++s) {
+      T left[REP];
 #pragma unroll
       for (int r = 0; r < REP; ++r) {
-        const int i = ci * REP + r;
-        T lft = left[r];
-        T cor = r == 0 ? corner_prev : left[r - 1];
-        // Columns c >= J (padding of the lane straddling J, and lanes past it) are updated too: the
-        // solution only flows right and down, so they never reach a real cell, and the lane's last
-        // column hands its value only to lanes that are all padding.
-#pragma unroll
-        for (int w = 0; w < W; ++w) {
-          const T upw = up[w];
-          T kn;
-          if constexpr (s1) {
-            kn = (upw + lft) * A[w / REP] - cor * B[w / REP];
-          } else {
-            kn = (upw + lft) + cor * B[w / REP];
-            if (hybrid && lane * W + w == i) {
-              const T inc = A[w / REP], inc2 = inc * inc;
-              kn = (upw + lft) * ((T)1 + (T)0.5 * inc + (T)(1.0 / 12) * inc2) - cor * ((T)1 - (T)(1.0 / 12) * inc2);
-            }
-          }
-          cor = upw;
-          lft = kn;
-          up[w] = kn;
-        }
-        last[r] = lft;
+        left[r] = lane_prev(last[r]);
+        if (lane == 0) left[r] = from_left ? bnd[min(s * REP + r + 1, I)] : (T)1;
       }
+      const int ci = s - lane;
+      if (ci >= 0 && ci < IC && lane < lanes_used) {
+        const float *dxr = dxs + ci * DP;
+        float dxv[DP];
+#pragma unroll
+        for (int k = 0; k < DP; ++k) dxv[k] = dxr[k];
+        // coefficients of the lane's coarse cells: solver 1 uses (A, B), solver 0 uses inc - 1 (as B)
+        T A[WC], B[WC];
+#pragma unroll
+        for (int w = 0; w < WC; ++w) {
+          float incf = 0.0f;
+#pragma unroll
+          for (int k = 0; k < DP; ++k) incf = __builtin_fmaf(dxv[k], dy[w][k], incf);
+          const T inc = (T)incf * inv_factor;
+          const T inc2 = inc * inc;
+          if constexpr (s1) {
+            A[w] = (T)1 + (T)0.5 * inc + (T)(1.0 / 12) * inc2;
+            B[w] = (T)1 - (T)(1.0 / 12) * inc2;
+          } else {
+            A[w] = inc;  // hybrid diagonal cells need inc
+            B[w] = inc - (T)1;
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < REP; ++r) {
+          const int i = ci * REP + r;
+          T lft = left[r];
+          T cor = r == 0 ? corner_prev : left[r - 1];
+          // Columns c >= J (padding of the lane straddling J, and lanes past it) are updated too: the
+          // solution only flows right and down, so they never reach a real cell, and the lane's last
+          // column hands its value only to lanes that are all padding.
+#pragma unroll
+          for (int w = 0; w < W; ++w) {
+            const T upw = up[w];
+            T kn;
+            if constexpr (s1) {
+              kn = (upw + lft) * A[w / REP] - cor * B[w / REP];
+            } else {
+              kn = (upw + lft) + cor * B[w / REP];
+              if (hybrid && c0 + lane * W + w == i) {
+                const T inc = A[w / REP], inc2 = inc * inc;
+                kn = (upw + lft) * ((T)1 + (T)0.5 * inc + (T)(1.0 / 12) * inc2) - cor * ((T)1 - (T)(1.0 / 12) * inc2);
+              }
+            }
+            cor = upw;
+            lft = kn;
+            up[w] = kn;
+          }
+          last[r] = lft;
+        }
+        if (to_right && lane == 63) {
+#pragma unroll
+          for (int r = 0; r < REP; ++r) bnd[ci * REP + r + 1] = last[r];
+        }
+      }
+      corner_prev = left[REP - 1];
     }
-    corner_prev = left[REP - 1];
   }
-  const int owner = (J - 1) / W, slot = (J - 1) % W;
+  const int c0 = (nblk - 1) * CB;
+  const int owner = (J - 1 - c0) / W, slot = (J - 1 - c0) % W;
   T res = (T)0;
 #pragma unroll
   for (int w = 0; w < W; ++w)
@@ -295,13 +312,23 @@ __global__ __launch_bounds__(256) void pde_rep_kernel(PdeArgs p) {
   }
 }
 
+// LDS of a pde_rep_kernel launch: the 4 waves' coarse x increments, then (column blocks only) their
+// boundary-column slabs
+template <typename T, int DP, int W, int REP>
+static size_t pde_rep_lds(int l1, int l2) {
+  const size_t dx = ((size_t)4 * (l1 - 1) * DP + 3) & ~(size_t)3;
+  const int J = REP * (l2 - 1);
+  const size_t bnd = J > 64 * W ? (size_t)4 * (REP * (l1 - 1) + 1) * sizeof(T) : 0;
+  return dx * sizeof(float) + bnd;
+}
+
 template <typename T, int DP, int W, int REP>
 static int launch_pde_rep(const PdeArgs &a, long long nblocks, hipStream_t s) {
   if constexpr ((W / REP) * DP > 64) {
     return -1;  // the per-row kernel keeps fewer increments in registers
   } else {
-    const size_t lds = (size_t)4 * (a.l1 - 1) * DP * sizeof(float);
-    if (lds > 64 * 1024) return GPSIG_EUNSUPPORTED;
+    const size_t lds = pde_rep_lds<T, DP, W, REP>(a.l1, a.l2);
+    if (lds > 160 * 1024) return GPSIG_EUNSUPPORTED;
     if (a.solver == 1)
       hipLaunchKernelGGL((pde_rep_kernel<T, DP, W, REP, 1>), dim3((unsigned)nblocks), dim3(256), lds, s, a);
     else
@@ -317,6 +344,8 @@ static int pde_rep_w(const PdeArgs &a, long long nblocks, int J, hipStream_t s) 
   if (J <= 128 * REP && 2 * REP <= 16) return launch_pde_rep<T, DP, (2 * REP <= 16 ? 2 * REP : REP), REP>(a, nblocks, s);
   if (REP <= 4 && J <= 192 * REP) return launch_pde_rep<T, DP, (REP <= 4 ? 3 * REP : REP), REP>(a, nblocks, s);
   if (REP <= 4 && J <= 256 * REP) return launch_pde_rep<T, DP, (REP <= 4 ? 4 * REP : REP), REP>(a, nblocks, s);
+  // longer: column blocks of 256 * REP fine columns
+  if (REP <= 4) return launch_pde_rep<T, DP, (REP <= 4 ? 4 * REP : REP), REP>(a, nblocks, s);
   return -1;
 }
 

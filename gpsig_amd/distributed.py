@@ -71,21 +71,14 @@ def _hip_assemble(gathered, row_off, level_stride, n, levels):
     return ops.sym_assemble(gathered, row_off, level_stride, n, levels)
 
 
-def sharded_sym_gram(X: torch.Tensor, num_levels: int, *, out_mode: int = L.OUT_NORM_SUM, group=None,
-                     compute=None, assemble=None, **kw) -> torch.Tensor:
-    """Full symmetric Gram on every rank.  kw: order, base, difference, rs1/rs2, scale, jitter.
-
-    Returns (n, n) for OUT_NORM_SUM, else (num_levels+1, n, n).
-    """
+def sym_local_blocks(X: torch.Tensor, num_levels: int, rank: int, world: int, *, out_mode: int = L.OUT_NORM_SUM,
+                     compute=None, **kw) -> torch.Tensor:
+    """Rank `rank`'s share of the symmetric Gram: its two row chunks r and 2P-1-r, (2, levels, B, n)
+    (chunk slot, level, row, column), rows past a chunk's end zero.  This is exactly the tensor the rank
+    contributes to the all-gather."""
     compute = compute or _hip_compute
-    assemble = assemble or _hip_assemble
-    rank, world = _world(group)
     n = X.shape[0]
     levels = 1 if out_mode == L.OUT_NORM_SUM else num_levels + 1
-    if world == 1:
-        out = torch.empty((levels, n, n), dtype=torch.float32, device=X.device)
-        compute(X, levels, (0, n), out, 0, num_levels=num_levels, out_mode=out_mode, **kw)
-        return out[0] if out_mode == L.OUT_NORM_SUM else out
     (a0, a1), (b0, b1), B = rank_chunks(n, world, rank)
     # (chunk slot, level, row, col): each chunk's block is contiguous for the kernel's output layout
     local = torch.zeros((2, levels, B, n), dtype=torch.float32, device=X.device)
@@ -93,17 +86,41 @@ def sharded_sym_gram(X: torch.Tensor, num_levels: int, *, out_mode: int = L.OUT_
         compute(X, levels, (a0, a1), local[0], a0, num_levels=num_levels, out_mode=out_mode, **kw)
     if b1 > b0:
         compute(X, levels, (b0, b1), local[1], b0, num_levels=num_levels, out_mode=out_mode, **kw)
-    gathered = torch.empty((world * 2 * levels * B, n), dtype=torch.float32, device=X.device)
-    dist.all_gather_into_tensor(gathered, local.reshape(2 * levels * B, n), group=group)
-    row_off = row_offsets(n, world, levels, device=X.device)
-    full = assemble(gathered, row_off, B * n, n, levels)
+    return local
+
+
+def sym_from_gathered(gathered: torch.Tensor, n: int, world: int, levels: int, assemble=None) -> torch.Tensor:
+    """Full (levels, n, n) symmetric Gram from the all-gathered (world * 2 * levels * B, n) buffer."""
+    assemble = assemble or _hip_assemble
+    _, B = triangle_chunks(n, world)
+    row_off = row_offsets(n, world, levels, device=gathered.device)
+    return assemble(gathered, row_off, B * n, n, levels)
+
+
+def sharded_sym_gram(X: torch.Tensor, num_levels: int, *, out_mode: int = L.OUT_NORM_SUM, group=None,
+                     compute=None, assemble=None, **kw) -> torch.Tensor:
+    """Full symmetric Gram on every rank.  kw: order, base, difference, rs1/rs2, scale, jitter.
+
+    Returns (n, n) for OUT_NORM_SUM, else (num_levels+1, n, n).
+    """
+    compute = compute or _hip_compute
+    rank, world = _world(group)
+    n = X.shape[0]
+    levels = 1 if out_mode == L.OUT_NORM_SUM else num_levels + 1
+    if world == 1:
+        out = torch.empty((levels, n, n), dtype=torch.float32, device=X.device)
+        compute(X, levels, (0, n), out, 0, num_levels=num_levels, out_mode=out_mode, **kw)
+        return out[0] if out_mode == L.OUT_NORM_SUM else out
+    local = sym_local_blocks(X, num_levels, rank, world, out_mode=out_mode, compute=compute, **kw)
+    gathered = torch.empty((world * local.numel() // n, n), dtype=torch.float32, device=X.device)
+    dist.all_gather_into_tensor(gathered, local.reshape(-1, n), group=group)
+    full = sym_from_gathered(gathered, n, world, levels, assemble)
     return full[0] if out_mode == L.OUT_NORM_SUM else full
 
 
-def sharded_cross_gram(X: torch.Tensor, X2: torch.Tensor, num_levels: int, *, out_mode: int = L.OUT_NORM_SUM,
-                       group=None, compute=None, **kw) -> torch.Tensor:
-    """K(X, X2) row-sharded over ranks; full (n1, n2) [or (levels, n1, n2)] on every rank."""
-    rank, world = _world(group)
+def cross_local_block(X: torch.Tensor, X2: torch.Tensor, num_levels: int, rank: int, world: int, *,
+                      out_mode: int = L.OUT_NORM_SUM, compute=None, **kw) -> torch.Tensor:
+    """Rank `rank`'s row block of K(X, X2): (levels, R, n2), R = ceil(n1 / world), rows past n1 zero."""
     n1, n2 = X.shape[0], X2.shape[0]
     levels = 1 if out_mode == L.OUT_NORM_SUM else num_levels + 1
     R = int(math.ceil(n1 / world))
@@ -114,12 +131,28 @@ def sharded_cross_gram(X: torch.Tensor, X2: torch.Tensor, num_levels: int, *, ou
             ops.sig_gram(X, X2, num_levels, rows=(r0, r1), out=local, out_row0=r0, out_mode=out_mode, **kw)
     else:
         compute(X, X2, levels, (r0, r1), local, r0, num_levels=num_levels, out_mode=out_mode, **kw)
+    return local
+
+
+def cross_from_gathered(g: torch.Tensor, n1: int) -> torch.Tensor:
+    """(levels, n1, n2) from the all-gathered (world, levels, R, n2) row blocks."""
+    world, levels, R, n2 = g.shape
+    return g.permute(1, 0, 2, 3).reshape(levels, world * R, n2)[:, :n1]
+
+
+def sharded_cross_gram(X: torch.Tensor, X2: torch.Tensor, num_levels: int, *, out_mode: int = L.OUT_NORM_SUM,
+                       group=None, compute=None, **kw) -> torch.Tensor:
+    """K(X, X2) row-sharded over ranks; full (n1, n2) [or (levels, n1, n2)] on every rank."""
+    rank, world = _world(group)
+    n1, n2 = X.shape[0], X2.shape[0]
+    local = cross_local_block(X, X2, num_levels, rank, world, out_mode=out_mode, compute=compute, **kw)
+    levels, R = local.shape[0], local.shape[1]
     if world == 1:
         full = local
     else:
         g = torch.empty((world, levels, R, n2), dtype=torch.float32, device=X.device)
         dist.all_gather_into_tensor(g.view(world * levels * R, n2), local.reshape(levels * R, n2), group=group)
-        full = g.permute(1, 0, 2, 3).reshape(levels, world * R, n2)[:, :n1]
+        full = cross_from_gathered(g, n1)
     return full[0] if out_mode == L.OUT_NORM_SUM else full
 
 

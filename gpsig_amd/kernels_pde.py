@@ -11,8 +11,10 @@ Differences from the reference, deliberately not reproduced (SURVEY.md section 2
     (kernels_pde.py:176-178); here both implementations use increments, as the Cython path does;
   * SignatureRBF/SignatureLinear pass ``order`` positionally into ``lengthscales``
     (kernels_pde.py:409,426); here ``order`` goes to ``order``;
-  * the 1024-point cap of the CUDA op (kernels_pde.py:53) becomes the gfx950 kernel's own limit,
-    2^order * (len-1) <= 1024 refined columns.
+  * the 1024-point cap of the CUDA op (kernels_pde.py:53) is gone for both implementations, as for the
+    reference's Cython path: the gfx950 solver sweeps long grids in column blocks (dyadic order <= 2;
+    bounded by the LDS for the boundary columns, about 4700 refined rows); the gradient keeps
+    2^order * (len-1) <= 1024 refined columns (GpsigError beyond).
 """
 from __future__ import annotations
 
@@ -24,7 +26,7 @@ from . import lags as _lags
 from . import ops
 from .kernels import DEFAULT_JITTER, _as_tensor, _tensor_inner_product, _tensor_logs
 
-PDE_MAX_COLUMNS = 1024
+PDE_MAX_COLUMNS = 1024  # refined columns of the gradient kernel (gpsig_pde_vjp)
 
 
 class UntruncSignatureKernel:
@@ -43,8 +45,6 @@ class UntruncSignatureKernel:
         assert implementation in ['cython', 'gpu_op'], "implementation should be 'cython' or 'gpu_op'"
         self.implementation = implementation
         self.order = order
-        assert (2 ** self.order) * (self.len_examples - 1) <= PDE_MAX_COLUMNS, \
-            "discretization level of the PDE solver too large for the gfx950 kernel"
         self.sigma = torch.tensor(1.0, dtype=torch.float64)
         self.num_levels = num_levels
         self.jitter = float(jitter)

@@ -85,3 +85,35 @@ def test_carry_too_large_raises():
     X = torch.zeros((2, 6000, 2), device=DEV)  # 4 waves x 5999 rows x 7 levels x 4 B > 160 KiB of LDS
     with pytest.raises(Lb.GpsigError):
         ops.sig_gram(X, None, 8)
+
+
+@pytest.mark.parametrize("L,n,solver", [(500, 2, 1), (500, 2, 0), (300, 2, 1), (600, 1, 1), (1200, 0, 1), (257, 2, 1)])
+def test_long_pde_matches_oracle(L, n, solver):
+    """Goursat PDE beyond 64 W refined columns (column blocks of pde_rep_kernel, boundary column in LDS):
+    L = 500 at dyadic 2 is 1996 refined columns, which the reference's gpu_op refuses
+    (kernels_pde.py:53) and its Cython path (sigKer_fast.pyx:15-62) solves; here both the diagonal
+    (solver 0 takes the solver-1 update on the diagonal, sigKer_fast.pyx:59) and the cross Gram vs the
+    C restatement (oracle/pde), which is bitwise the reference's Cython solver (tests/test_oracle.py)."""
+    from oracle import pde
+    from gpsig_amd import ops
+    rng = np.random.default_rng(L + n)
+    X = np.cumsum(rng.standard_normal((3, L, 4)), 1) / np.sqrt(L * 4) * 2
+    Y = np.cumsum(rng.standard_normal((2, L - 11, 4)), 1) / np.sqrt(L * 4) * 2
+    got = ops.pde_diag(t(X), n, solver).cpu().numpy()
+    exp = pde.pde_diag(X, n, solver)
+    assert np.abs(got - exp).max() / np.abs(exp).max() < TOL
+    if solver == 1:
+        assert norm_rel_err(ops.pde_gram(t(X), t(Y), n, 1).cpu().numpy(), pde.pde_gram(X, Y, n, 1)) < TOL
+        assert norm_rel_err(ops.pde_gram(t(X), None, n, 1).cpu().numpy(), pde.pde_gram(X, X, n, 1)) < TOL
+
+
+def test_long_pde_kernel_class_kdiag():
+    """UntruncSignatureKernel(order=2).Kdiag at L = 500 (the reference's gpu_op asserts here)."""
+    import gpsig_amd
+    from oracle import pde
+    L, D = 500, 3
+    X = walks(4, L, D, 9) * 2
+    k = gpsig_amd.UntruncSignatureKernel(L * D, D, order=2)
+    got = k.Kdiag(t(X.reshape(4, -1))).cpu().numpy()
+    exp = pde.pde_diag(X, 2, 1)
+    assert np.abs(got - exp).max() / np.abs(exp).max() < TOL
