@@ -44,6 +44,7 @@ _SZ = ctypes.c_size_t
 
 SIGNATURES = {
     "gpsig_sig_workspace_bytes": (_SZ, [_I, _I, _I, _I, _I]),
+    "gpsig_sig_vjp_workspace_bytes": (_SZ, [_I, _I, _I, _I, _I, _I, _I]),
     "gpsig_sig_gram": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I,
                             _P, _P, _P, _F, _I, _P, _I, _I, _P, _SZ, _P]),
     "gpsig_sig_diag": (_I, [_P, _I, _I, _I, _I, _I, _I, _I, _F, _I, _P, _P, _SZ, _P]),

@@ -41,7 +41,25 @@ struct BwdArgs {
   float jitter;
   float *gX, *gY, *grs1, *grs2, *gscale;
   const float *state;  // optional saved forward state (RECT / UPPER), see gpsig_sig_gram_state
+  // column blocks (LP = 64, sequences longer than one lane group covers): per-pair scratch of
+  // scr_stride floats at scratch + (blockIdx.x * 4 + wave) * scr_stride, see bwd_scratch_floats
+  int nblk;
+  long long blk0;  // first logical workgroup of this launch (the host splits blocked launches)
+  float *scratch;
+  long long scr_stride;
 };
+
+// Load of a carry another lane of this wave stored earlier in the launch: served by L2 (agent scope),
+// never by a possibly stale vector L1 line.
+GPSIG_DEV float ld_l2(const float *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
+
+// Scratch of one pair in column-block mode (floats): the forward carries into blocks 1..nblk-1
+// (nrows x (M-1) each), the adjoint carry slab (nrows x (M-1)), the end-of-sweep column sums of every
+// block ((M-1) x W x 64, lane-minor).
+__host__ __device__ inline long long bwd_scratch_floats(int nrows, int M, int W, int nblk) {
+  if (nblk <= 1 || M <= 1) return 0;
+  return (long long)nblk * nrows * (M - 1) + (long long)nblk * (M - 1) * W * 64;
+}
 
 // Exclusive scan over the group's columns of per-lane column arrays v[W] (W columns of lane gl hold
 // columns gl*W .. gl*W+W-1), N independent arrays, scans step-interleaved.
@@ -94,6 +112,57 @@ GPSIG_DEV void group_rexcl_cols_n(const float (&v)[N][W], float (&out)[N][W]) {
   }
 }
 
+// Column-block variants (LP = 64): add a wave-uniform carry cin[n] to every exclusive prefix and return
+// the group total of v in tot[n] (wave-uniform), for the next block's carry.
+template <int W, int N>
+GPSIG_DEV void wave_excl_cols_carry_n(const float (&v)[N][W], float (&out)[N][W], const float (&cin)[N],
+                                      float (&tot)[N]) {
+  float t[N], incl[N];
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    float s = 0.0f;
+#pragma unroll
+    for (int w = 0; w < W; ++w) s += v[n][w];
+    t[n] = s;
+    incl[n] = s;
+  }
+  group_incl_scan_n<64, N>(incl);
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    tot[n] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, incl[n]), 63));
+    float run = incl[n] - t[n] + cin[n];
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      out[n][w] = run;
+      run += v[n][w];
+    }
+  }
+}
+template <int W, int N>
+GPSIG_DEV void wave_rexcl_cols_carry_n(const float (&v)[N][W], float (&out)[N][W], const float (&cin)[N],
+                                       float (&tot)[N]) {
+  float t[N], incl[N];
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    float s = 0.0f;
+#pragma unroll
+    for (int w = 0; w < W; ++w) s += v[n][w];
+    t[n] = s;
+    incl[n] = s;
+  }
+  group_incl_scan_n<64, N>(incl);
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    tot[n] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, incl[n]), 63));
+    float run = tot[n] - incl[n] + cin[n];  // sum over the lanes after this one, plus the blocks to the right
+#pragma unroll
+    for (int w = W - 1; w >= 0; --w) {
+      out[n][w] = run;
+      run += v[n][w];
+    }
+  }
+}
+
 // Sum over the whole wave of N values; the result is valid in lane 63.
 template <int N>
 GPSIG_DEV void wave_sum_last_n(float (&v)[N]) {
@@ -114,28 +183,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
   constexpr int RC = W >= 4 ? 4 : 8;  // rows per chunk of the reverse sweep (<= the forward's anchor period)
   __shared__ __attribute__((aligned(16))) float cbuf[RBF && DIFF ? 4 : 1][RBF && DIFF ? RC : 1][64][2 * W];
   constexpr int ML = M > 1 ? M - 1 : 1;
+  constexpr int CPB = LP * W - 1;  // cells of a column block (the last lane's last column is its halo point)
 
   const int lane = threadIdx.x & 63;
   const int wave = wave_uniform(threadIdx.x >> 6);
   const int g = lane / LP;
   const int gl = lane % LP;
   const bool diag = p.pair_mode == GPSIG_PAIRS_DIAG;
+  const long long lblk = p.blk0 + (long long)blockIdx.x;  // logical workgroup
 
   // ---- which pair (same enumeration as sig_fo_kernel)
   int a, b;
   if (diag) {
-    a = p.row_begin + (int)blockIdx.x * 4 + wave;
+    a = p.row_begin + (int)lblk * 4 + wave;
     b = a;
     if (a >= p.row_end) return;
   } else {
     int ta, tb;
     if (p.pair_mode == GPSIG_PAIRS_UPPER) {
-      const Tile t = upper_tile(p.tile_base + (long long)blockIdx.x, p.ntb, 4 / G);
+      const Tile t = upper_tile(p.tile_base + lblk, p.ntb, 4 / G);
       ta = t.ta;
       tb = t.tb;
     } else {
-      ta = p.tiles_a0 + (int)blockIdx.x / p.ntb;
-      tb = (int)blockIdx.x % p.ntb;
+      ta = p.tiles_a0 + (int)(lblk / p.ntb);
+      tb = (int)(lblk % p.ntb);
     }
     a = ta * 4 + wave;
     b = tb * G + g;
@@ -150,24 +221,40 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
   const float *__restrict__ fx = p.FX + (long long)a * l1 * FS;
   cfloat *fxc = as_const(fx);  // row records: scalar loads, independent of the atomics below
   const float *__restrict__ fy = p.FY + (long long)bl * l2 * FS;
+  const int nrows = DIFF ? l1 - 1 : l1;
 
-  // ---- column data of this lane
+  // ---- column blocks: block k holds the cells j0 .. j0 + CPB - 1 on the points j0 .. j0 + CPB (j0 = k CPB)
+  const int nblk = (LP == 64) ? p.nblk : 1;
+  const bool blocked = LP == 64 && nblk > 1 && M > 1;
+  float *__restrict__ scr = blocked ? p.scratch + ((long long)blockIdx.x * 4 + wave) * p.scr_stride : nullptr;
+  // forward carry into block k (k >= 1): [i][m] = sum_{j < j0} C_{m+1}(i, j) before row i
+  auto tcar = [&](int k) { return scr + (long long)(k - 1) * nrows * ML; };
+  float *__restrict__ ucar = blocked ? scr + (long long)(nblk - 1) * nrows * ML : nullptr;  // adjoint carry slab
+  auto endst = [&](int k) { return ucar + (long long)nrows * ML + (long long)k * ML * W * 64; };
+
+  // ---- column data of this lane in block k
   float y[W][DP], dy[W][DP], hdy[W];
   bool colv[W], ptv[W];
+  int j0 = 0;
+  auto load_cols = [&](int blk) {
+    j0 = blk * CPB;
+    // points of this block: the DIFF seeds see the halo point, the point seeds do not
+    const int npts = nblk == 1 ? l2 : min(l2 - j0, DIFF ? CPB + 1 : CPB);
 #pragma unroll
-  for (int w = 0; w < W; ++w) {
-    const int j = gl * W + w;
-    colv[w] = j < (DIFF ? l2 - 1 : l2);  // columns of the grid the recursion consumes
-    ptv[w] = j < l2;
-    const int jj = j < l2 ? j : l2 - 1;
-    const float *f = fy + (long long)jj * FS;
+    for (int w = 0; w < W; ++w) {
+      const int j = gl * W + w;
+      colv[w] = j < (DIFF ? npts - 1 : npts);  // columns of the grid the recursion consumes
+      ptv[w] = j < npts;
+      const int jj = j0 + (j < npts ? j : npts - 1);
+      const float *f = fy + (long long)jj * FS;
 #pragma unroll
-    for (int k = 0; k < DP; ++k) {
-      y[w][k] = f[k];
-      dy[w][k] = f[DP + k];
+      for (int k = 0; k < DP; ++k) {
+        y[w][k] = f[k];
+        dy[w][k] = f[DP + k];
+      }
+      hdy[w] = f[2 * DP];
     }
-    hdy[w] = f[2 * DP];
-  }
+  };
 
   // k(x_i, y_j) of one point row (RBF); identical instructions in both sweeps
   auto krow = [&](cfloat *xr, float (&k)[W]) {
@@ -217,18 +304,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
       }
     }
   };
-
-  // ---- forward sweep, or its end state saved by the forward launch (gpsig_sig_gram_state)
-  float C[M][W];
-#pragma unroll
-  for (int m = 0; m < M; ++m)
-#pragma unroll
-    for (int w = 0; w < W; ++w) C[m][w] = 0.0f;
-  float kc[W], kcR = 0.0f;
-  float K[M + 1];
-  K[0] = 1.0f;
-  const int nrows = DIFF ? l1 - 1 : l1;
-  const bool saved = DIFF && p.state != nullptr;  // kernel-uniform (the host passes state for DIFF only)
   // difference=False: the cells are the point grid itself, k(x_i, y_j) (signature_algs.py:26 skipped)
   auto point_cells = [&](int i, float (&dM)[W], float (&k0)[W]) {
     cfloat *xr = fxc + (long long)i * FS;
@@ -250,24 +325,28 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
       }
     }
   };
-  if (saved) {
-    const int nc = l2 - 1;
-    const float *__restrict__ st =
-        p.state + (pair_ok ? state_slot(a, bl, p.n2, p.pair_mode == GPSIG_PAIRS_UPPER) * state_stride(M, l2) : 0);
+
+  // ---- forward sweep(s), or the end state saved by the forward launch (gpsig_sig_gram_state)
+  float C[M][W];
+  float kc[W], kcR = 0.0f;
+  float K[M + 1];
+  K[0] = 1.0f;
+  const bool saved = DIFF && p.state != nullptr;  // kernel-uniform (the host passes state for DIFF only)
+  auto zeroC = [&]() {
 #pragma unroll
-    for (int m = 0; m + 1 < M; ++m)
+    for (int m = 0; m < M; ++m)
 #pragma unroll
-      for (int w = 0; w < W; ++w) {
-        const int j = gl * W + w;
-        C[m][w] = (pair_ok && j < nc) ? st[(long long)m * nc + j] : 0.0f;
-      }
+      for (int w = 0; w < W; ++w) C[m][w] = 0.0f;
+  };
+  zeroC();
+  // blocks whose forward sweep runs: all (no saved state), or those left of the last (their carries)
+  const int nfwd = saved ? (blocked ? nblk - 1 : 0) : nblk;
+  float Kacc[M];
 #pragma unroll
-    for (int m = 1; m <= M; ++m) K[m] = pair_ok ? st[(long long)(M - 1) * nc + m - 1] : 0.0f;
-    if constexpr (RBF) {
-      krow(fxc + (long long)nrows * FS, kc);  // k row of the last point, as the sweep would leave it
-      kcR = lane_next(kc[0]);
-    }
-  } else {
+  for (int m = 0; m < M; ++m) Kacc[m] = 0.0f;
+  for (int blk = 0; blk < nfwd; ++blk) {
+    load_cols(blk);
+    zeroC();
     if constexpr (RBF && DIFF) {
       krow(fxc, kc);
       kcR = lane_next(kc[0]);
@@ -290,7 +369,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
         for (int m = 0; m < ML; ++m)
 #pragma unroll
           for (int w = 0; w < W; ++w) Cs[m][w] = C[m][w];
-        group_excl_cols_n<LP, W, ML>(Cs, S);
+        if (blocked) {
+          float cin[ML], tot[ML];
+#pragma unroll
+          for (int m = 0; m < ML; ++m) cin[m] = blk > 0 ? ld_l2(tcar(blk) + (long long)i * ML + m) : 0.0f;
+          wave_excl_cols_carry_n<W, ML>(Cs, S, cin, tot);
+          if (blk + 1 < nblk && lane == 0) {
+#pragma unroll
+            for (int m = 0; m < ML; ++m) tcar(blk + 1)[(long long)i * ML + m] = cin[m] + tot[m];
+          }
+        } else {
+          group_excl_cols_n<LP, W, ML>(Cs, S);
+        }
 #pragma unroll
         for (int m = 1; m < M; ++m)
 #pragma unroll
@@ -304,14 +394,30 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
         kcR = knR;
       }
     }
-
+    if (!saved) {
 #pragma unroll
-    for (int m = 0; m < M; ++m) {
-      float s = 0.0f;
+      for (int m = 0; m < M; ++m) {
+        float s = 0.0f;
 #pragma unroll
-      for (int w = 0; w < W; ++w) s += C[m][w];
-      K[m + 1] = group_sum<LP>(s);
+        for (int w = 0; w < W; ++w) s += C[m][w];
+        Kacc[m] += group_sum<LP>(s);
+      }
+      if (blocked) {  // this block's end state, for its reverse sweep
+#pragma unroll
+        for (int m = 0; m < ML; ++m)
+#pragma unroll
+          for (int w = 0; w < W; ++w) endst(blk)[((long long)m * W + w) * 64 + lane] = C[m][w];
+      }
     }
+  }
+  if (saved) {
+    const float *__restrict__ st =
+        p.state + (pair_ok ? state_slot(a, bl, p.n2, p.pair_mode == GPSIG_PAIRS_UPPER) * state_stride(M, l2) : 0);
+#pragma unroll
+    for (int m = 1; m <= M; ++m) K[m] = pair_ok ? st[(long long)(M - 1) * (l2 - 1) + m - 1] : 0.0f;
+  } else {
+#pragma unroll
+    for (int m = 0; m < M; ++m) K[m + 1] = Kacc[m];
     if constexpr (DIFF) K[1] = level1_closed<DP, SEED>(fx, fy, l1, l2);
   }
 
@@ -360,256 +466,312 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
     }
   }
 
-  // ---- reverse sweep
-  float Ch[ML][W];
-#pragma unroll
-  for (int m = 0; m < ML; ++m)
-#pragma unroll
-    for (int w = 0; w < W; ++w) Ch[m][w] = gw[m + 1];
-  const float gM = gw[M];
-  float Ep[W], A[W], B[W][DP];
-#pragma unroll
-  for (int w = 0; w < W; ++w) {
-    Ep[w] = 0.0f;
-    A[w] = 0.0f;
-#pragma unroll
-    for (int k = 0; k < DP; ++k) B[w][k] = 0.0f;
-  }
+  // ---- reverse sweep, blocks right to left
   float *__restrict__ gxa = p.gX + (long long)a * l1 * p.d;
   const int d = p.d;
-
-  // point row `pi` of the grid receives dLoss/dk(x_pi, y_j) = Kh[w]: x-gradient reduced over the wave
-  // (all pairs of a wave share a), y-gradient accumulated per column
-  auto emit = [&](int pi, const float (&Kh)[W], const float (&kr)[W]) {
-    cfloat *xp = fxc + (long long)pi * FS;
-    float xi[DP];
+  const float gM = gw[M];
+  for (int blk = nblk - 1; blk >= 0; --blk) {
+    const bool cin_left = blocked && blk > 0;          // forward carry from the blocks to the left
+    const bool uin_right = blocked && blk + 1 < nblk;  // adjoint carry from the blocks to the right
+    const bool uout_left = blocked && blk > 0;
+    if (nfwd != 1 || nblk > 1) load_cols(blk);  // (single unsaved block: still loaded from the forward)
+    if (saved) {
+      const int nc = l2 - 1;
+      const float *__restrict__ st =
+          p.state + (pair_ok ? state_slot(a, bl, p.n2, p.pair_mode == GPSIG_PAIRS_UPPER) * state_stride(M, l2) : 0);
 #pragma unroll
-    for (int k = 0; k < DP; ++k) xi[k] = xp[k];
-    float wg[W];
-#pragma unroll
-    for (int w = 0; w < W; ++w) {
-      const float v = RBF ? Kh[w] * kr[w] : Kh[w];
-      wg[w] = ptv[w] ? v : 0.0f;
-    }
-    float s[DP + 1];
-#pragma unroll
-    for (int k = 0; k <= DP; ++k) s[k] = 0.0f;
-#pragma unroll
-    for (int w = 0; w < W; ++w) {
-      s[DP] += wg[w];
-#pragma unroll
-      for (int k = 0; k < DP; ++k) s[k] = __builtin_fmaf(wg[w], y[w][k], s[k]);
-      A[w] += wg[w];
-#pragma unroll
-      for (int k = 0; k < DP; ++k) B[w][k] = __builtin_fmaf(wg[w], xi[k], B[w][k]);
-    }
-    wave_sum_last_n<DP + 1>(s);
-    if (lane == 63) {
-#pragma unroll
-      for (int k = 0; k < DP; ++k) {  // compile-time indices (a runtime bound would put s, xi in scratch)
-        const float v = RBF ? __builtin_fmaf(-s[DP], xi[k], s[k]) : s[k];
-        if (k < d) unsafeAtomicAdd(gxa + (long long)pi * d + k, v);
-      }
-    }
-  };
-
-  float kr1[W];  // k row of point i+1 (DIFF)
-  if constexpr (RBF && DIFF) {
-#pragma unroll
-    for (int w = 0; w < W; ++w) kr1[w] = kc[w];
-  } else {
-#pragma unroll
-    for (int w = 0; w < W; ++w) kr1[w] = 1.0f;
-  }
-  // one row of the reverse sweep from its cells dM(i, .) and the k row of point i
-  auto rev_row = [&](int i, const float (&dM)[W], const float (&k0)[W]) {
-    // forward state of row i: C_m(i) = C_m(i+1) - dM S_{m-1}(i), ascending levels (C[m] holds level m+1,
-    // S_0 = 1), and dLoss/d dM(i, j) = sum_m Ch_m(i+1, j) S_{m-1}(i, j)
-    float Dh[W];
-#pragma unroll
-    for (int w = 0; w < W; ++w) {
-      C[0][w] -= dM[w];
-      Dh[w] = (M > 1) ? Ch[0][w] : gM;
-    }
-#pragma unroll
-    for (int s = 1; s < M; ++s) {
-      float Cm[1][W], Sm[1][W];
-#pragma unroll
-      for (int w = 0; w < W; ++w) Cm[0][w] = C[s - 1][w];
-      group_excl_cols_n<LP, W, 1>(Cm, Sm);  // S_s(i) from the recovered C_s(i)
-#pragma unroll
-      for (int w = 0; w < W; ++w) {
-        if (s + 1 < M) C[s][w] = __builtin_fmaf(-dM[w], Sm[0][w], C[s][w]);
-        const float chn = (s + 1 < M) ? Ch[s < ML ? s : 0][w] : gM;  // Ch_{s+1}
-        Dh[w] = __builtin_fmaf(chn, Sm[0][w], Dh[w]);
-      }
-    }
-#pragma unroll
-    for (int w = 0; w < W; ++w) Dh[w] = colv[w] ? Dh[w] : 0.0f;
-
-    // adjoint column sums: Ch_m(i) = Ch_m(i+1) + rexcl(dM * Ch_{m+1}(i+1)), ascending m (old Ch_{m+1})
-    if constexpr (M > 1) {
-      float v[ML][W], r[ML][W];
-#pragma unroll
-      for (int m = 0; m < ML; ++m)
-#pragma unroll
-        for (int w = 0; w < W; ++w) v[m][w] = dM[w] * ((m + 1 < ML) ? Ch[m + 1][w] : gM);
-      group_rexcl_cols_n<LP, W, ML>(v, r);
-#pragma unroll
-      for (int m = 0; m < ML; ++m)
-#pragma unroll
-        for (int w = 0; w < W; ++w) Ch[m][w] += r[m][w];
-    }
-
-    if constexpr (DIFF) {
-      // adjoint of the second difference: E(i, j) = Dh(i, j-1) - Dh(i, j); Kh(i+1, j) = E(i, j) - E(i+1, j)
-      float left = lane_prev(Dh[W - 1]);
-      if (gl == 0) left = 0.0f;
-      float Kh[W];
-#pragma unroll
-      for (int w = 0; w < W; ++w) {
-        const float e = ((w == 0) ? left : Dh[w - 1]) - Dh[w];
-        Kh[w] = e - Ep[w];
-        Ep[w] = e;
-      }
-      emit(i + 1, Kh, kr1);
-#pragma unroll
-      for (int w = 0; w < W; ++w) kr1[w] = k0[w];
-    } else {
-      emit(i, Dh, k0);  // the cell is the point value: dLoss/dk(x_i, y_j) = Dh(i, j)
-    }
-  };
-
-  if constexpr (RBF && DIFF) {
-    // Chunked: the cells of RC rows are regenerated forward from an exact row (k and expm1(q) from
-    // x - y) with the exp-free recurrences of the forward kernel (sig_common.h RbfSeedPk; chunk
-    // starts at multiples of RC <= its anchor period, so the cells are the forward launch's) into
-    // this lane's LDS slots, then consumed in reverse.  Cells with |p| or |c| >= EM1_TAU take the
-    // corner difference of the k grid with an exact next row (wave-uniform branch).
-    float(*cb)[64][2 * W] = cbuf[wave];
-    auto exact_row = [&](cfloat *xr, float (&k)[W], float (&Eq)[W]) {
-      float xv[DP];
-#pragma unroll
-      for (int c = 0; c < DP; ++c) xv[c] = xr[c];
-#pragma unroll
-      for (int w = 0; w < W; ++w) {
-        float s2 = 0.0f, q = -hdy[w];
-#pragma unroll
-        for (int c = 0; c < DP; ++c) {
-          const float df = xv[c] - y[w][c];
-          s2 = __builtin_fmaf(df, df, s2);
-          q = __builtin_fmaf(df, dy[w][c], q);
-        }
-        k[w] = __builtin_amdgcn_exp2f(s2 * NHL2E);
-        Eq[w] = __builtin_fabsf(q) < EM1_TAU ? em1_small(q) : __builtin_amdgcn_exp2f(q * L2E) - 1.0f;
-      }
-    };
-    auto chunk_fwd = [&](int i0, int nr) {
-      float kc[W], Eq[W];
-      exact_row(fxc + (long long)i0 * FS, kc, Eq);
-      for (int r = 0; r < nr; ++r) {
-        cfloat *fr = fxc + (long long)(i0 + r) * FS;
-        float dxv[DP];
-#pragma unroll
-        for (int c = 0; c < DP; ++c) dxv[c] = fr[DP + c];
-        const float g = fr[2 * DP + 1];
-        float dM[W], kn[W], Eqn[W], mx[W];
-        bool slow = false;
+      for (int m = 0; m + 1 < M; ++m)
 #pragma unroll
         for (int w = 0; w < W; ++w) {
-          float pp = -g, c = 0.0f;
-#pragma unroll
-          for (int k = 0; k < DP; ++k) {
-            pp = __builtin_fmaf(y[w][k], dxv[k], pp);
-            c = __builtin_fmaf(dy[w][k], dxv[k], c);
-          }
-          const float Ep = em1_small(pp), Ec = em1_small(c);
-          float t = __builtin_fmaf(Ep, Ec, Ec);
-          t = __builtin_fmaf(Eq[w], t, t);
-          dM[w] = kc[w] * __builtin_fmaf(Ep, Eq[w], t);
-          kn[w] = __builtin_fmaf(kc[w], Ep, kc[w]);
-          Eqn[w] = __builtin_fmaf(Eq[w], Ec, Eq[w] + Ec);
-          mx[w] = __builtin_fmaxf(__builtin_fabsf(pp), __builtin_fabsf(c));
-          slow = slow || !(mx[w] < EM1_TAU);
+          const int jl = gl * W + w, j = j0 + jl;
+          C[m][w] = (pair_ok && j < nc && jl < CPB) ? st[(long long)m * nc + j] : 0.0f;
         }
-        if (__builtin_amdgcn_ballot_w64(slow) != 0) {
-          exact_row(fr + FS, kn, Eqn);
-          const float knR = lane_next(kn[0]), kcR2 = lane_next(kc[0]);
+    } else if (blocked) {
+#pragma unroll
+      for (int m = 0; m < ML; ++m)
+#pragma unroll
+        for (int w = 0; w < W; ++w) C[m][w] = endst(blk)[((long long)m * W + w) * 64 + lane];
+    }
+    if constexpr (RBF && DIFF) {
+      if (saved || nblk > 1) {
+        krow(fxc + (long long)nrows * FS, kc);  // k row of the last point, as the sweep would leave it
+        kcR = lane_next(kc[0]);
+      }
+    }
+
+    float Ch[ML][W];
+#pragma unroll
+    for (int m = 0; m < ML; ++m)
+#pragma unroll
+      for (int w = 0; w < W; ++w) Ch[m][w] = gw[m + 1];
+    float Ep[W], A[W], B[W][DP];
+#pragma unroll
+    for (int w = 0; w < W; ++w) {
+      Ep[w] = 0.0f;
+      A[w] = 0.0f;
+#pragma unroll
+      for (int k = 0; k < DP; ++k) B[w][k] = 0.0f;
+    }
+
+    // point row `pi` of the grid receives dLoss/dk(x_pi, y_j) = Kh[w]: x-gradient reduced over the wave
+    // (all pairs of a wave share a), y-gradient accumulated per column
+    auto emit = [&](int pi, const float (&Kh)[W], const float (&kr)[W]) {
+      cfloat *xp = fxc + (long long)pi * FS;
+      float xi[DP];
+#pragma unroll
+      for (int k = 0; k < DP; ++k) xi[k] = xp[k];
+      float wg[W];
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        const float v = RBF ? Kh[w] * kr[w] : Kh[w];
+        wg[w] = ptv[w] ? v : 0.0f;
+      }
+      float s[DP + 1];
+#pragma unroll
+      for (int k = 0; k <= DP; ++k) s[k] = 0.0f;
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        s[DP] += wg[w];
+#pragma unroll
+        for (int k = 0; k < DP; ++k) s[k] = __builtin_fmaf(wg[w], y[w][k], s[k]);
+        A[w] += wg[w];
+#pragma unroll
+        for (int k = 0; k < DP; ++k) B[w][k] = __builtin_fmaf(wg[w], xi[k], B[w][k]);
+      }
+      wave_sum_last_n<DP + 1>(s);
+      if (lane == 63) {
+#pragma unroll
+        for (int k = 0; k < DP; ++k) {  // compile-time indices (a runtime bound would put s, xi in scratch)
+          const float v = RBF ? __builtin_fmaf(-s[DP], xi[k], s[k]) : s[k];
+          if (k < d) unsafeAtomicAdd(gxa + (long long)pi * d + k, v);
+        }
+      }
+    };
+
+    float kr1[W];  // k row of point i+1 (DIFF)
+    if constexpr (RBF && DIFF) {
+#pragma unroll
+      for (int w = 0; w < W; ++w) kr1[w] = kc[w];
+    } else {
+#pragma unroll
+      for (int w = 0; w < W; ++w) kr1[w] = 1.0f;
+    }
+    // one row of the reverse sweep from its cells dM(i, .) and the k row of point i
+    auto rev_row = [&](int i, const float (&dM)[W], const float (&k0)[W]) {
+      // forward state of row i: C_m(i) = C_m(i+1) - dM S_{m-1}(i), ascending levels (C[m] holds level m+1,
+      // S_0 = 1), and dLoss/d dM(i, j) = sum_m Ch_m(i+1, j) S_{m-1}(i, j)
+      float Dh[W];
+#pragma unroll
+      for (int w = 0; w < W; ++w) {
+        C[0][w] -= dM[w];
+        Dh[w] = (M > 1) ? Ch[0][w] : gM;
+      }
+#pragma unroll
+      for (int s = 1; s < M; ++s) {
+        float Cm[1][W], Sm[1][W];
+#pragma unroll
+        for (int w = 0; w < W; ++w) Cm[0][w] = C[s - 1][w];
+        if (blocked) {
+          float cin[1], tot[1];
+          cin[0] = cin_left ? ld_l2(tcar(blk) + (long long)i * ML + s - 1) : 0.0f;
+          wave_excl_cols_carry_n<W, 1>(Cm, Sm, cin, tot);
+        } else {
+          group_excl_cols_n<LP, W, 1>(Cm, Sm);  // S_s(i) from the recovered C_s(i)
+        }
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          if (s + 1 < M) C[s][w] = __builtin_fmaf(-dM[w], Sm[0][w], C[s][w]);
+          const float chn = (s + 1 < M) ? Ch[s < ML ? s : 0][w] : gM;  // Ch_{s+1}
+          Dh[w] = __builtin_fmaf(chn, Sm[0][w], Dh[w]);
+        }
+      }
+#pragma unroll
+      for (int w = 0; w < W; ++w) Dh[w] = colv[w] ? Dh[w] : 0.0f;
+
+      // adjoint column sums: Ch_m(i) = Ch_m(i+1) + rexcl(dM * Ch_{m+1}(i+1)), ascending m (old Ch_{m+1})
+      if constexpr (M > 1) {
+        float v[ML][W], r[ML][W];
+#pragma unroll
+        for (int m = 0; m < ML; ++m)
+#pragma unroll
+          for (int w = 0; w < W; ++w) v[m][w] = dM[w] * ((m + 1 < ML) ? Ch[m + 1][w] : gM);
+        if (blocked) {
+          float uin[ML], tot[ML];
+          float *__restrict__ ur = ucar + (long long)i * ML;
+#pragma unroll
+          for (int m = 0; m < ML; ++m) uin[m] = uin_right ? ld_l2(ur + m) : 0.0f;
+          wave_rexcl_cols_carry_n<W, ML>(v, r, uin, tot);
+          if (uout_left && lane == 0) {
+#pragma unroll
+            for (int m = 0; m < ML; ++m) ur[m] = uin[m] + tot[m];
+          }
+        } else {
+          group_rexcl_cols_n<LP, W, ML>(v, r);
+        }
+#pragma unroll
+        for (int m = 0; m < ML; ++m)
+#pragma unroll
+          for (int w = 0; w < W; ++w) Ch[m][w] += r[m][w];
+      }
+
+      if constexpr (DIFF) {
+        // adjoint of the second difference: E(i, j) = Dh(i, j-1) - Dh(i, j); Kh(i+1, j) = E(i, j) - E(i+1, j)
+        float left = lane_prev(Dh[W - 1]);
+        if (gl == 0) left = 0.0f;
+        float Kh[W];
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          const float e = ((w == 0) ? left : Dh[w - 1]) - Dh[w];
+          Kh[w] = e - Ep[w];
+          Ep[w] = e;
+        }
+        emit(i + 1, Kh, kr1);
+#pragma unroll
+        for (int w = 0; w < W; ++w) kr1[w] = k0[w];
+      } else {
+        emit(i, Dh, k0);  // the cell is the point value: dLoss/dk(x_i, y_j) = Dh(i, j)
+      }
+    };
+
+    if constexpr (RBF && DIFF) {
+      // Chunked: the cells of RC rows are regenerated forward from an exact row (k and expm1(q) from
+      // x - y) with the exp-free recurrences of the forward kernel (sig_common.h RbfSeedPk; chunk
+      // starts at multiples of RC <= its anchor period, so the cells are the forward launch's) into
+      // this lane's LDS slots, then consumed in reverse.  Cells with |p| or |c| >= EM1_TAU take the
+      // corner difference of the k grid with an exact next row (wave-uniform branch).
+      float(*cb)[64][2 * W] = cbuf[wave];
+      auto exact_row = [&](cfloat *xr, float (&k)[W], float (&Eq)[W]) {
+        float xv[DP];
+#pragma unroll
+        for (int c = 0; c < DP; ++c) xv[c] = xr[c];
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          float s2 = 0.0f, q = -hdy[w];
+#pragma unroll
+          for (int c = 0; c < DP; ++c) {
+            const float df = xv[c] - y[w][c];
+            s2 = __builtin_fmaf(df, df, s2);
+            q = __builtin_fmaf(df, dy[w][c], q);
+          }
+          k[w] = __builtin_amdgcn_exp2f(s2 * NHL2E);
+          Eq[w] = __builtin_fabsf(q) < EM1_TAU ? em1_small(q) : __builtin_amdgcn_exp2f(q * L2E) - 1.0f;
+        }
+      };
+      auto chunk_fwd = [&](int i0, int nr) {
+        float kc[W], Eq[W];
+        exact_row(fxc + (long long)i0 * FS, kc, Eq);
+        for (int r = 0; r < nr; ++r) {
+          cfloat *fr = fxc + (long long)(i0 + r) * FS;
+          float dxv[DP];
+#pragma unroll
+          for (int c = 0; c < DP; ++c) dxv[c] = fr[DP + c];
+          const float g = fr[2 * DP + 1];
+          float dM[W], kn[W], Eqn[W], mx[W];
+          bool slow = false;
 #pragma unroll
           for (int w = 0; w < W; ++w) {
-            const float kn1 = (w + 1 < W) ? kn[w + 1] : knR;
-            const float kc1 = (w + 1 < W) ? kc[w + 1] : kcR2;
-            if (!(mx[w] < EM1_TAU)) dM[w] = (kn1 - kn[w]) - (kc1 - kc[w]);
+            float pp = -g, c = 0.0f;
+#pragma unroll
+            for (int k = 0; k < DP; ++k) {
+              pp = __builtin_fmaf(y[w][k], dxv[k], pp);
+              c = __builtin_fmaf(dy[w][k], dxv[k], c);
+            }
+            const float Ep = em1_small(pp), Ec = em1_small(c);
+            float t = __builtin_fmaf(Ep, Ec, Ec);
+            t = __builtin_fmaf(Eq[w], t, t);
+            dM[w] = kc[w] * __builtin_fmaf(Ep, Eq[w], t);
+            kn[w] = __builtin_fmaf(kc[w], Ep, kc[w]);
+            Eqn[w] = __builtin_fmaf(Eq[w], Ec, Eq[w] + Ec);
+            mx[w] = __builtin_fmaxf(__builtin_fabsf(pp), __builtin_fabsf(c));
+            slow = slow || !(mx[w] < EM1_TAU);
+          }
+          if (__builtin_amdgcn_ballot_w64(slow) != 0) {
+            exact_row(fr + FS, kn, Eqn);
+            const float knR = lane_next(kn[0]), kcR2 = lane_next(kc[0]);
+#pragma unroll
+            for (int w = 0; w < W; ++w) {
+              const float kn1 = (w + 1 < W) ? kn[w + 1] : knR;
+              const float kc1 = (w + 1 < W) ? kc[w + 1] : kcR2;
+              if (!(mx[w] < EM1_TAU)) dM[w] = (kn1 - kn[w]) - (kc1 - kc[w]);
+            }
+          }
+#pragma unroll
+          for (int w = 0; w < W; ++w) {
+            cb[r][lane][w] = colv[w] ? dM[w] : 0.0f;
+            cb[r][lane][W + w] = kc[w];
+            kc[w] = kn[w];
+            Eq[w] = Eqn[w];
           }
         }
+      };
+      for (int i0 = ((nrows - 1) / RC) * RC; i0 >= 0; i0 -= RC) {
+        const int nr = nrows - i0 < RC ? nrows - i0 : RC;
+        chunk_fwd(i0, nr);
+        for (int r = nr - 1; r >= 0; --r) {
+          float dM[W], k0[W];
 #pragma unroll
-        for (int w = 0; w < W; ++w) {
-          cb[r][lane][w] = colv[w] ? dM[w] : 0.0f;
-          cb[r][lane][W + w] = kc[w];
-          kc[w] = kn[w];
-          Eq[w] = Eqn[w];
+          for (int w = 0; w < W; ++w) {
+            dM[w] = cb[r][lane][w];
+            k0[w] = cb[r][lane][W + w];
+          }
+          rev_row(i0 + r, dM, k0);
         }
       }
-    };
-    for (int i0 = ((nrows - 1) / RC) * RC; i0 >= 0; i0 -= RC) {
-      const int nr = nrows - i0 < RC ? nrows - i0 : RC;
-      chunk_fwd(i0, nr);
-      for (int r = nr - 1; r >= 0; --r) {
-        float dM[W], k0[W];
+    } else if constexpr (DIFF) {
+      for (int i = nrows - 1; i >= 0; --i) {
+        float k0[W], dM[W];
 #pragma unroll
-        for (int w = 0; w < W; ++w) {
-          dM[w] = cb[r][lane][w];
-          k0[w] = cb[r][lane][W + w];
-        }
-        rev_row(i0 + r, dM, k0);
+        for (int w = 0; w < W; ++w) k0[w] = 1.0f;
+        cells(fxc + (long long)i * FS, k0, kr1, 0.0f, 0.0f, dM);
+        rev_row(i, dM, k0);
+      }
+    } else {
+      for (int i = nrows - 1; i >= 0; --i) {
+        float k0[W], dM[W];
+        point_cells(i, dM, k0);
+        rev_row(i, dM, k0);
       }
     }
-  } else if constexpr (DIFF) {
-    for (int i = nrows - 1; i >= 0; --i) {
-      float k0[W], dM[W];
+    if constexpr (DIFF) {
+      float Kh[W];
 #pragma unroll
-      for (int w = 0; w < W; ++w) k0[w] = 1.0f;
-      cells(fxc + (long long)i * FS, k0, kr1, 0.0f, 0.0f, dM);
-      rev_row(i, dM, k0);
+      for (int w = 0; w < W; ++w) Kh[w] = -Ep[w];
+      emit(0, Kh, kr1);
     }
-  } else {
-    for (int i = nrows - 1; i >= 0; --i) {
-      float k0[W], dM[W];
-      point_cells(i, dM, k0);
-      rev_row(i, dM, k0);
-    }
-  }
-  if constexpr (DIFF) {
-    float Kh[W];
-#pragma unroll
-    for (int w = 0; w < W; ++w) Kh[w] = -Ep[w];
-    emit(0, Kh, kr1);
-  }
 
-  // ---- y-gradient of the pair's columns
-  if (pair_ok) {
-    float *__restrict__ gyb = (diag ? p.gX : p.gY) + (long long)bl * l2 * d;
+    // ---- y-gradient of the block's points
+    if (pair_ok) {
+      float *__restrict__ gyb = (diag ? p.gX : p.gY) + (long long)bl * l2 * d;
 #pragma unroll
-    for (int w = 0; w < W; ++w) {
-      const int j = gl * W + w;
-      if (!ptv[w]) continue;
+      for (int w = 0; w < W; ++w) {
+        const int j = j0 + gl * W + w;
+        if (!ptv[w]) continue;
 #pragma unroll
-      for (int k = 0; k < DP; ++k) {
-        const float v = RBF ? __builtin_fmaf(-A[w], y[w][k], B[w][k]) : B[w][k];
-        if (k < d) unsafeAtomicAdd(gyb + (long long)j * d + k, v);
+        for (int k = 0; k < DP; ++k) {
+          const float v = RBF ? __builtin_fmaf(-A[w], y[w][k], B[w][k]) : B[w][k];
+          if (k < d) unsafeAtomicAdd(gyb + (long long)j * d + k, v);
+        }
       }
     }
   }
 }
 
 // Column geometry of the backward kernel: W columns per lane, LP lanes per pair.  The lane keeps
-// y, dy and the y-gradient accumulator (3 W DP floats) plus 2 (M-1) W level states.
+// y, dy and the y-gradient accumulator (3 W DP floats) plus 2 (M-1) W level states.  Longer sequences
+// run at LP = 64 in column blocks of 64 W - 1 cells (BwdArgs::nblk).
 struct BwdGeo { int W, LP; };
 inline BwdGeo bwd_geometry(int l2, int DP) {
   const int W = DP <= 8 ? 4 : 2;
   for (int LP : {16, 32, 64})
     if (LP * W >= l2) return {W, LP};
-  return {0, 0};
+  return {W, 64};
 }
+inline int bwd_blocks(int l2, bool diff, BwdGeo g) {
+  if (g.LP * g.W >= l2) return 1;
+  const int cells = diff ? l2 - 1 : l2, cpb = g.LP * g.W - 1;
+  return (cells + cpb - 1) / cpb;
+}
+// workgroups per launch of a column-block VJP (4 pairs each): bounds the per-pair scratch
+constexpr long long BWD_CHUNK_BLOCKS = 2048;
 
 }  // namespace gpsig

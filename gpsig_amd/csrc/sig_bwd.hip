@@ -61,11 +61,14 @@ extern "C" int gpsig_sig_gram_vjp(const float *X, int n1, int l1, const float *Y
   const BwdGeo geo = bwd_geometry(l2, DP);
   if (geo.W == 0 || num_levels > 8) return GPSIG_EUNSUPPORTED;
   if (row_end == row_begin) return GPSIG_OK;
+  const int nblk = bwd_blocks(l2, difference != 0, geo);
+  const long long scr_stride = bwd_scratch_floats(difference ? l1 - 1 : l1, num_levels, geo.W, nblk);
 
   const bool same = (X == Y && n1 == n2 && l1 == l2);
   const size_t fx_b = align256((size_t)n1 * l1 * feat_stride(DP) * sizeof(float));
   const size_t fy_b = same ? 0 : align256((size_t)n2 * l2 * feat_stride(DP) * sizeof(float));
-  if (!workspace || workspace_bytes < fx_b + fy_b) return GPSIG_EWORKSPACE;
+  const size_t scr_b = (size_t)scr_stride * 4 * BWD_CHUNK_BLOCKS * sizeof(float);
+  if (!workspace || workspace_bytes < fx_b + fy_b + scr_b) return GPSIG_EWORKSPACE;
   float *FX = static_cast<float *>(workspace);
   float *FY = same ? FX : reinterpret_cast<float *>(static_cast<char *>(workspace) + fx_b);
   int rc = features(X, n1, l1, d, DP, FX, s);
@@ -92,6 +95,9 @@ extern "C" int gpsig_sig_gram_vjp(const float *X, int n1, int l1, const float *Y
   a.grs2 = pair_mode == GPSIG_PAIRS_RECT ? grs2 : grs1;
   a.gscale = gscale;
   a.state = state;
+  a.nblk = nblk;
+  a.scratch = scr_stride ? reinterpret_cast<float *>(static_cast<char *>(workspace) + fx_b + fy_b) : nullptr;
+  a.scr_stride = scr_stride;
 
   const int G = 64 / geo.LP;
   long long nblocks;
@@ -112,11 +118,29 @@ extern "C" int gpsig_sig_gram_vjp(const float *X, int n1, int l1, const float *Y
   }
   if (nblocks > 0x7fffffffLL) return GPSIG_EUNSUPPORTED;
   if (nblocks <= 0) return GPSIG_OK;
-  switch (DP) {
+  // column-block launches go in chunks of BWD_CHUNK_BLOCKS workgroups (the scratch holds one chunk)
+  const long long chunk = scr_stride ? BWD_CHUNK_BLOCKS : nblocks;
+  for (long long c = 0; c < nblocks; c += chunk) {
+    a.blk0 = c;
+    const long long nb = nblocks - c < chunk ? nblocks - c : chunk;
+    switch (DP) {
 #define CASE(v) \
-  case v: return bwd_dp<v>(a, seed, nblocks, s);
-    CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(8) CASE(16)
+  case v: rc = bwd_dp<v>(a, seed, nb, s); break;
+      CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(8) CASE(16)
 #undef CASE
-    default: return GPSIG_EUNSUPPORTED;
+      default: return GPSIG_EUNSUPPORTED;
+    }
+    if (rc) return rc;
   }
+  return GPSIG_OK;
+}
+
+extern "C" size_t gpsig_sig_vjp_workspace_bytes(int n1, int l1, int n2, int l2, int d, int num_levels, int difference) {
+  const int DP = bwd_pad(d);
+  if (DP == 0 || n1 <= 0 || n2 <= 0 || l1 < 1 || l2 < 1) return 0;
+  const BwdGeo geo = bwd_geometry(l2, DP);
+  const int nblk = bwd_blocks(l2, difference != 0, geo);
+  const long long scr = bwd_scratch_floats(difference ? l1 - 1 : l1, num_levels, geo.W, nblk);
+  return align256((size_t)n1 * l1 * feat_stride(DP) * sizeof(float)) +
+         align256((size_t)n2 * l2 * feat_stride(DP) * sizeof(float)) + (size_t)scr * 4 * BWD_CHUNK_BLOCKS * sizeof(float);
 }

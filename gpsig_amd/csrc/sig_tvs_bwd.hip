@@ -20,7 +20,7 @@ __global__ __launch_bounds__(256) void tvs_gx_add_kernel(const float *__restrict
 }
 
 static size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
-static int tvs_bwd_pad(int d) { return d <= 2 ? 2 : d <= 4 ? 4 : d <= 6 ? 6 : d <= 8 ? 8 : 0; }
+static int tvs_bwd_pad(int d) { return d <= 2 ? 2 : d <= 4 ? 4 : d <= 6 ? 6 : d <= 8 ? 8 : d <= 12 ? 12 : d <= 16 ? 16 : 0; }
 
 }  // namespace gpsig
 
@@ -59,6 +59,10 @@ extern "C" int gpsig_tens_vs_seq_vjp(const float *Z, int lt, int t, int incremen
     case 13: rc = tvs_bwd_launch_dp<6, true>(a, num_levels, rbf, difference != 0, s); break;
     case 16: rc = tvs_bwd_launch_dp<8, false>(a, num_levels, rbf, difference != 0, s); break;
     case 17: rc = tvs_bwd_launch_dp<8, true>(a, num_levels, rbf, difference != 0, s); break;
+    case 24: rc = tvs_bwd_launch_dp<12, false>(a, num_levels, rbf, difference != 0, s); break;
+    case 25: rc = tvs_bwd_launch_dp<12, true>(a, num_levels, rbf, difference != 0, s); break;
+    case 32: rc = tvs_bwd_launch_dp<16, false>(a, num_levels, rbf, difference != 0, s); break;
+    case 33: rc = tvs_bwd_launch_dp<16, true>(a, num_levels, rbf, difference != 0, s); break;
     default: return GPSIG_EUNSUPPORTED;
   }
   if (rc) return rc;

@@ -188,7 +188,7 @@ def sig_gram_vjp(X: torch.Tensor, Y: torch.Tensor | None, num_levels: int, gout:
         rs1, rs2 = _f32(rs1), _f32(rs2)
     if scale is not None:
         scale = _f32(scale)
-    nb = lib.gpsig_sig_workspace_bytes(n1, l1, n2, l2, d)
+    nb = lib.gpsig_sig_vjp_workspace_bytes(n1, l1, n2, l2, d, num_levels, int(bool(difference)))
     ws = workspace(X.device, nb)
     mode = L.PAIRS_DIAG if diag else (L.PAIRS_UPPER if sym else L.PAIRS_RECT)
     rc = lib.gpsig_sig_gram_vjp(X.data_ptr(), n1, l1, Y.data_ptr(), n2, l2, d, num_levels, base_kind(base),

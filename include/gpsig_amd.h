@@ -124,8 +124,11 @@ int gpsig_sig_diag(const float *X, int n, int l, int d, int num_levels, int orde
  *   grs1 (L+1, n1), grs2 (L+1, n2) = dLoss/drs (the host chains them through rs = (diag+jitter)^-1/2
  *   into a DIAG call); gscale (L+1) = dLoss/dscale.  Any of grs1/grs2/gscale may be NULL.
  *   state: NULL, or the buffer a gpsig_sig_gram_state call with the same inputs filled (RECT/UPPER).
- *   Workspace: gpsig_sig_workspace_bytes(n1, l1, n2, l2, d).
+ *   Workspace: gpsig_sig_vjp_workspace_bytes(n1, l1, n2, l2, d, num_levels, difference): the feature
+ *   records, and for sequences longer than one lane group covers (column blocks) the per-row carries of
+ *   one launch chunk.  Any length; d <= 16.
  */
+size_t gpsig_sig_vjp_workspace_bytes(int n1, int l1, int n2, int l2, int d, int num_levels, int difference);
 int gpsig_sig_gram_vjp(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int num_levels,
                        int base_kind, int difference, int pair_mode, int row_begin, int row_end, const float *gout, int gout_levels,
                        const float *rs1, const float *rs2, const float *scale, float jitter, float *gX, float *gY,
@@ -163,7 +166,7 @@ int gpsig_tens_gram(const float *Z, int lt, int t, int increments, int d, int nu
 int gpsig_tens_gram_vjp(const float *Z, int lt, int t, int increments, int d, int num_levels, int base_kind,
                         const float *gout, float *gZ, gpsig_stream_t stream);
 
-/* Gradient of gpsig_tens_vs_seq (order 1, difference 1 or 0, RBF or linear, num_levels <= 8, d <= 8):
+/* Gradient of gpsig_tens_vs_seq (order 1, difference 1 or 0, RBF or linear, num_levels <= 8, d <= 16):
  * the reference differentiates _K_tens_vs_seq (kernels.py:314-341 + signature_algs.py:101-127) by TF
  * autodiff.  gout (num_levels+1, T, n) = dLoss/d(raw per-level output); accumulates (+=) gZ (same
  * layout as Z) and gX (n, l, d).  Workspace: gpsig_tens_vjp_workspace_bytes(n, l, d). */
