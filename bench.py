@@ -130,7 +130,7 @@ def main():
                     help="RBF seed dots on packed VALU FMAs (default) or on the matrix cores (A/B arm)")
     ap.add_argument("--backend", default="nccl",
                     help="process-group backend (nccl = RCCL; gloo only to rehearse N>1 ranks on one GPU)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r1_gram_counters.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r2_gram_counters.json"),
                     help="per-launch HBM bytes of the Gram kernel from a PMC pass (profiles/*.json)")
     args = ap.parse_args()
 
@@ -241,7 +241,7 @@ def main():
                      "kernel": "sig_fo_kernel", "seed_engine": args.seed_engine, "launch_ms": avg_launch_s * 1e3, "bytes_per_entry": b_entry,
                      "entries_per_launch": entries_per_launch,
                      # the fused kernel never materialises the tile: physically it is VALU-issue bound
-                     "physical_bound": "valu", "valu_issue_util": prof.get("valu_issue_util"),
+                     "physical_bound": "valu", "valu_busy": prof.get("valu_busy"),
                      "profile": os.path.relpath(args.traffic_json, ROOT) if prof else None,
                      # the datasheet peak and a measured device-to-device copy, both
                      "peak_probe": probe, "frac_probe": achieved / probe if probe else None},

@@ -22,8 +22,8 @@ here = os.path.dirname(os.path.abspath(__file__))
 
 
 def is_gram(name):
-    # sig_fo_kernel<DP, W, LP, M, SEED, DIAGK = false, SAVE = false>
-    return "sig_fo_kernel" in name and ("false, false>" in name or "Lb0ELb0E" in name)
+    # sig_fo_kernel<DP, W, LP, M, SEED, DIAGK = false, SAVE = false, MF = false>
+    return "sig_fo_kernel" in name and ("false, false, false>" in name or "Lb0ELb0ELb0E" in name)
 
 
 def one(pattern):
@@ -52,10 +52,21 @@ out = {
     "hbm_bytes_per_launch": (2 * avg["FETCH_SIZE"] + avg["WRITE_SIZE"]) * 1024 if "FETCH_SIZE" in avg else None,
     "note": "FETCH_SIZE/WRITE_SIZE in KiB; FETCH doubled per MI355X_MICROARCH.md (gfx950 tallies 128-B reads at 64 B)",
 }
-if "SQ_INSTS_VALU" in avg and "GRBM_GUI_ACTIVE" in avg and gram_stats:
-    # VALU issue utilisation: wave-instructions x 4 cycles (wave64 on a 16-lane SIMD) over SIMD-cycles
-    cycles = avg["GRBM_GUI_ACTIVE"] / 8  # summed over the 8 XCDs
-    out["valu_issue_util"] = avg["SQ_INSTS_VALU"] * 4 / (cycles * 1024)
+if "GRBM_GUI_ACTIVE" in avg and gram_stats:
+    cycles = avg["GRBM_GUI_ACTIVE"] / 8  # summed over the 8 XCDs: shader cycles of the launch
     out["effective_clock_ghz"] = cycles / (out["avg_duration_ms"] * 1e6)
+    simd_cycles = cycles * 1024  # 256 CUs x 4 SIMDs
+    if "SQ_ACTIVE_INST_VALU" in avg:
+        # measured busy counter (quad-cycles, MI355X_MICROARCH.md PMC units): fraction of the SIMDs'
+        # cycles with a VALU instruction executing
+        out["valu_busy"] = avg["SQ_ACTIVE_INST_VALU"] * 4 / simd_cycles
+    if "SQ_VALU_MFMA_BUSY_CYCLES" in avg:
+        out["mfma_busy"] = avg["SQ_VALU_MFMA_BUSY_CYCLES"] / simd_cycles
+    if "SQ_WAVE_CYCLES" in avg:
+        for k in ("SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY"):
+            if k in avg:
+                out[k.lower().replace("sq_", "") + "_per_wave_cycle"] = avg[k] / avg["SQ_WAVE_CYCLES"]
+    if "SQ_INSTS_VALU" in avg:
+        out["valu_insts_x4_over_simd_cycles"] = avg["SQ_INSTS_VALU"] * 4 / simd_cycles
 json.dump(out, open(os.path.join(here, f"{tag}_gram_counters.json"), "w"), indent=1)
 print(json.dumps(out, indent=1))
