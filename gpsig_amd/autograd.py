@@ -14,8 +14,10 @@ When a gradient is needed, the forward Gram launch also saves its end-of-sweep s
 sweep; above GRAM_STATE_BYTES (env GPSIG_GRAM_STATE_BYTES) the VJP recomputes it instead.
 
 Gradients reach the sequences (and, through the host-side scaling in kernels.py, the lengthscales)
-and sigma * variances.  Supported for order == 1 (difference True or False); higher orders evaluate
-forward but raise NotImplementedError on backward.
+and sigma * variances.  Supported for order == 1 (difference True or False), and for the Gram and its
+diagonal of SignatureLinear with order >= num_levels (the exact signature kernel; backward through the
+signature features, ops.sig_gram_ho_vjp); other higher orders evaluate forward but raise
+NotImplementedError on backward.
 """
 from __future__ import annotations
 
@@ -30,11 +32,57 @@ from . import ops
 GRAM_STATE_BYTES = int(os.environ.get("GPSIG_GRAM_STATE_BYTES", 16 << 30))
 
 
+def _ho_signature_case(cfg):
+    """Higher order with the linear base kernel and order >= num_levels (the exact signature kernel,
+    as benchmarks/models/train_gpsig_vosf.py:102 trains it): differentiable through signature features."""
+    return cfg["order"] >= cfg["num_levels"] and cfg["base"] in ("linear", "lin") and cfg["difference"]
+
+
 def _check_bwd(cfg, gram=False):
-    """The VJP kernels cover order 1 (difference True or False)."""
-    if cfg["order"] != 1:
+    """The VJP kernels cover order 1 (difference True or False); Gram / diagonal gradients of higher
+    orders are covered for the exact signature kernel (linear, order >= num_levels)."""
+    if cfg["order"] != 1 and not (gram and _ho_signature_case(cfg)):
         raise NotImplementedError("gradients of the signature kernels are implemented for order=1 "
-                                  "(gpsig_sig_gram_vjp, gpsig_tens_vs_seq_vjp)")
+                                  "(gpsig_sig_gram_vjp, gpsig_tens_vs_seq_vjp) and, for the Gram and its "
+                                  "diagonal, for SignatureLinear with order >= num_levels")
+
+
+def _ho_gram_backward(ctx, gout):
+    """Backward of SigGram for the higher-order signature case: the fused epilogue (jitter, 1/sqrt(diag)
+    normalisation, sigma * variances, level sum) is restated in torch on the raw levels and differentiated
+    there; the raw levels and diagonals go through ops.sig_gram_ho_vjp."""
+    cfg = ctx.cfg
+    Xs, X2s, sc32, rs1, rs2 = ctx.saved_tensors
+    M = cfg["num_levels"]
+    sym = X2s is None
+    kw = dict(order=cfg["order"], base=cfg["base"], difference=cfg["difference"])
+    with torch.enable_grad():
+        Kr = ops.sig_gram(Xs.detach(), None if sym else X2s.detach(), M, **kw).double().requires_grad_(True)
+        sc = sc32.double().requires_grad_(True)
+        ins = [Kr, sc]
+        if cfg["normalization"] and sym:  # kernels.py:431-434: K += jitter I, divide by its diagonal
+            n = Kr.shape[1]
+            Kj = Kr + cfg["jitter"] * torch.eye(n, dtype=Kr.dtype, device=Kr.device)[None]
+            dd = torch.sqrt(torch.diagonal(Kj, dim1=1, dim2=2))
+            K = Kj / (dd[:, :, None] * dd[:, None, :])
+        elif cfg["normalization"]:  # kernels.py:457-470: the two raw diagonals + jitter
+            d1 = ops.sig_diag(Xs.detach(), M, **kw).double().requires_grad_(True)
+            d2 = ops.sig_diag(X2s.detach(), M, **kw).double().requires_grad_(True)
+            ins += [d1, d2]
+            K = Kr / (torch.sqrt(d1 + cfg["jitter"])[:, :, None] * torch.sqrt(d2 + cfg["jitter"])[:, None, :])
+        else:
+            K = Kr
+        K = K * sc[:, None, None]
+        out = K if cfg["return_levels"] else K.sum(0)
+        grads = torch.autograd.grad(out, ins, gout.double())
+    gK, gsc = grads[0], grads[1]
+    gd1 = grads[2] if len(grads) > 2 else None
+    gd2 = grads[3] if len(grads) > 3 else None
+    gX, gY = ops.sig_gram_ho_vjp(Xs.detach(), None if sym else X2s.detach(), M, gK, gd1, gd2)
+    gXo = gX.to(Xs.dtype) if ctx.needs_input_grad[0] else None
+    gYo = gY.to(X2s.dtype) if (not sym and ctx.needs_input_grad[1]) else None
+    gso = gsc.to(ctx.scale_dtype) if ctx.needs_input_grad[2] else None
+    return gXo, gYo, gso, None
 
 
 class SigGram(torch.autograd.Function):
@@ -69,6 +117,8 @@ class SigGram(torch.autograd.Function):
     def backward(ctx, gout):
         cfg = ctx.cfg
         _check_bwd(cfg, gram=True)
+        if cfg["order"] != 1:
+            return _ho_gram_backward(ctx, gout)
         Xs, X2s, sc32, rs1, rs2 = ctx.saved_tensors
         M = cfg["num_levels"]
         sym = X2s is None
@@ -114,8 +164,11 @@ class SigDiag(torch.autograd.Function):
         cfg = ctx.cfg
         _check_bwd(cfg, gram=True)
         (Xs,) = ctx.saved_tensors
-        gX, _ = ops.sig_gram_vjp(Xs.detach(), None, cfg["num_levels"], gout, base=cfg["base"], diag=True,
-                                 difference=cfg["difference"])
+        if cfg["order"] != 1:
+            gX, _ = ops.sig_gram_ho_vjp(Xs.detach(), None, cfg["num_levels"], None, gout)
+        else:
+            gX, _ = ops.sig_gram_vjp(Xs.detach(), None, cfg["num_levels"], gout, base=cfg["base"], diag=True,
+                                     difference=cfg["difference"])
         return gX.to(Xs.dtype), None
 
 

@@ -282,6 +282,45 @@ def pde_gram_vjp(X: torch.Tensor, Y: torch.Tensor | None, gout: torch.Tensor, dy
 
 
 # ----------------------------------------------------------------------------- signature features
+def sig_gram_ho_vjp(X: torch.Tensor, Y: torch.Tensor | None, num_levels: int, gK: torch.Tensor | None,
+                    gd1: torch.Tensor | None = None, gd2: torch.Tensor | None = None):
+    """dLoss/dX, dLoss/dY of the raw per-level higher-order Gram of the linear base kernel with
+    order >= num_levels (signature_algs.py:37-74 over kernels.py:979-986; the configuration
+    benchmarks/models/train_gpsig_vosf.py:102 trains).  There the recursion is exactly the inner product of
+    truncated signatures, K_m(x, y) = <S_m(x), S_m(y)> (tests/golden/linear_chen.npz pins it), so the VJP
+    goes through the signature features: dLoss/dS_m(x_a) = sum_b gK_m(a, b) S_m(y_b) (+ 2 gd1_m(a) S_m(x_a)
+    for the raw diagonal), then the gfx950 signature VJP (gpsig_signature_vjp).
+
+    gK (M+1, n1, n2) = dLoss/dK_m for K(X, Y), or for the symmetric K(X) when Y is None; gd1 (M+1, n1),
+    gd2 (M+1, n2) = dLoss/d(raw diagonal) of X and Y.  Returns (gX, gY) float32 (gY None when Y is None).
+    """
+    M = num_levels
+    X = _f32(X)
+    n1, l1, d = X.shape
+    PX = signature(X, M)
+    sizes = [d ** m for m in range(1, M + 1)]
+    offs = [sum(sizes[:m]) for m in range(M + 1)]
+    PY = PX if Y is None else signature(_f32(Y), M)
+    gPX = torch.zeros_like(PX)
+    gPY = None if Y is None else torch.zeros_like(PY)
+    for m in range(1, M + 1):
+        sl = slice(offs[m - 1], offs[m])
+        if gK is not None:
+            g = gK[m].to(torch.float32)
+            if Y is None:
+                gPX[:, sl] += (g + g.T) @ PX[:, sl]
+            else:
+                gPX[:, sl] += g @ PY[:, sl]
+                gPY[:, sl] += g.T @ PX[:, sl]
+        if gd1 is not None:
+            gPX[:, sl] += 2.0 * gd1[m].to(torch.float32)[:, None] * PX[:, sl]
+        if gd2 is not None and Y is not None:
+            gPY[:, sl] += 2.0 * gd2[m].to(torch.float32)[:, None] * PY[:, sl]
+    gX = signature_vjp(X, M, gPX)
+    gY = None if Y is None else signature_vjp(_f32(Y), M, gPY)
+    return gX, gY
+
+
 def signature(X: torch.Tensor, depth: int) -> torch.Tensor:
     """Truncated signatures, levels 1..depth flattened first-index-major (iisignature.sig layout):
     X (n, l, d) -> (n, sum_m d^m) float32."""

@@ -8,7 +8,8 @@ The reference has no hand-written gradient for the truncated signature kernel: S
 differentiates K through TF-1.15 autodiff of the graph (file:line relative to /root/reference)
 
   * base kernels                 gpsig/kernels.py:946-957 (_square_dist), :979-986 (_lin), :1042-1044 (_rbf)
-  * second difference + recursion gpsig/signature_algs.py:8-35 (signature_kern_first_order)
+  * second difference + recursion gpsig/signature_algs.py:8-35 (signature_kern_first_order),
+                                 :37-74 (signature_kern_higher_order)
   * scaling                      gpsig/kernels.py:344-365 (X / lengthscales; num_lags=0)
   * K: jitter, normalisation by sqrt(diag), sigma*variances, level sum   gpsig/kernels.py:402-477
   * Kdiag (unnormalised)         gpsig/kernels.py:510-541
@@ -57,28 +58,54 @@ def first_order(M: torch.Tensor, num_levels: int, difference: bool = True) -> to
     return torch.stack(K, 0)
 
 
-def k_seq(Xs, X2s, num_levels, base="rbf", difference=True):
-    """_K_seq (kernels.py:209-238) for order 1: Xs (n1,l1,d), X2s (n2,l2,d) or None."""
+def higher_order(M: torch.Tensor, num_levels: int, order: int, difference: bool = True) -> torch.Tensor:
+    """signature_algs.py:37-74 on a 4-D (n1, l1, n2, l2) tensor -> (num_levels+1, n1, n2): the d x d
+    array of tensors R with the 1/j, 1/(jk) corrections, cumsums over axis 1 (x time) and -1 (y time)."""
+    K = [torch.ones((M.shape[0], M.shape[2]), dtype=M.dtype)]
+    if difference:
+        M = M[:, 1:, :, 1:] + M[:, :-1, :, :-1] - M[:, :-1, :, 1:] - M[:, 1:, :, :-1]
+    K.append(M.sum(dim=(1, -1)))
+    R = [[M]]
+    for i in range(2, num_levels + 1):
+        d = min(i, order)
+        Rn = [[None] * d for _ in range(d)]
+        Rn[0][0] = M * _xcumsum(_xcumsum(sum(r for row in R for r in row), 1), -1)
+        for j in range(2, d + 1):
+            Rn[0][j - 1] = M * _xcumsum(sum(R[a][j - 2] for a in range(len(R))), 1) / j
+            Rn[j - 1][0] = M * _xcumsum(sum(R[j - 2][b] for b in range(len(R))), -1) / j
+            for k in range(2, d + 1):
+                Rn[j - 1][k - 1] = M * R[j - 2][k - 2] / (j * k)
+        K.append(sum(r for row in Rn for r in row).sum(dim=(1, -1)))
+        R = Rn
+    return torch.stack(K, 0)
+
+
+def _recursion(M, num_levels, difference, order):
+    return first_order(M, num_levels, difference) if order == 1 else higher_order(M, num_levels, order, difference)
+
+
+def k_seq(Xs, X2s, num_levels, base="rbf", difference=True, order=1):
+    """_K_seq (kernels.py:209-238): Xs (n1,l1,d), X2s (n2,l2,d) or None."""
     n1, l1, d = Xs.shape
     Y = Xs if X2s is None else X2s
     n2, l2, _ = Y.shape
     M = base_kern(Xs.reshape(n1 * l1, d), Y.reshape(n2 * l2, d), base).reshape(n1, l1, n2, l2)
-    return first_order(M, num_levels, difference)
+    return _recursion(M, num_levels, difference, order)
 
 
-def k_seq_diag(Xs, num_levels, base="rbf", difference=True):
+def k_seq_diag(Xs, num_levels, base="rbf", difference=True, order=1):
     """_K_seq_diag (kernels.py:190-207): per-sequence (n, l, l) base kernel -> (num_levels+1, n)."""
     n, l, d = Xs.shape
     Ms = torch.stack([base_kern(Xs[a], Xs[a], base) for a in range(n)], 0)  # (n, l, l)
     M = Ms[:, :, None, :]  # run the 3-D branch as a (n, l, 1, l) tensor
-    K = first_order(M, num_levels, difference)  # (M+1, n, 1)
+    K = _recursion(M, num_levels, difference, order)  # (M+1, n, 1)
     return K[:, :, 0]
 
 
 def K(Xs, X2s, num_levels, base="rbf", normalization=True, scale=None, jitter=1e-6, return_levels=False,
-      difference=True):
+      difference=True, order=1):
     """SignatureKernel.K (kernels.py:402-477) on scaled sequences; scale = sigma * variances (M+1)."""
-    K_l = k_seq(Xs, X2s, num_levels, base, difference)
+    K_l = k_seq(Xs, X2s, num_levels, base, difference, order)
     if normalization:
         if X2s is None:
             n = Xs.shape[0]
@@ -86,8 +113,8 @@ def K(Xs, X2s, num_levels, base="rbf", normalization=True, scale=None, jitter=1e
             dsq = torch.sqrt(torch.diagonal(K_l, dim1=1, dim2=2))
             K_l = K_l / (dsq[:, :, None] * dsq[:, None, :])
         else:
-            d1 = torch.sqrt(k_seq_diag(Xs, num_levels, base, difference) + jitter)
-            d2 = torch.sqrt(k_seq_diag(X2s, num_levels, base, difference) + jitter)
+            d1 = torch.sqrt(k_seq_diag(Xs, num_levels, base, difference, order) + jitter)
+            d2 = torch.sqrt(k_seq_diag(X2s, num_levels, base, difference, order) + jitter)
             K_l = K_l / (d1[:, :, None] * d2[:, None, :])
     if scale is None:
         scale = torch.ones(num_levels + 1, dtype=K_l.dtype)

@@ -113,3 +113,22 @@ def test_autodiff_oracle_tens_gram(base, increments):
         m_[idx] -= h
         fd[idx] = ((k.K_tens_raw(p, increments) * G).sum() - (k.K_tens_raw(m_, increments) * G).sum()) / (2 * h)
     np.testing.assert_allclose(Zt.grad.numpy(), fd, rtol=1e-5, atol=1e-7)
+
+
+@pytest.mark.parametrize("base,order", [("linear", 5), ("linear", 2), ("rbf", 3)])
+def test_autodiff_oracle_higher_order_matches_numpy_oracle_and_chen(base, order):
+    """The torch restatement of signature_algs.py:37-74 equals the NumPy oracle; with the linear base
+    kernel and order = num_levels it is the exact signature kernel (Chen), the golden linear_chen.npz."""
+    from conftest import golden
+    M = 5
+    X, X2 = walks(4, 9, 2, 5), walks(3, 9, 2, 6)
+    k = kr.SignatureKernelRef(9 * 2, 2, M, base=base, order=order, normalization=False)
+    ref = k.K(X.reshape(4, -1), X2.reshape(3, -1), return_levels=True)
+    got = ar.K(torch.tensor(X), torch.tensor(X2), M, base=base, order=order, normalization=False,
+               return_levels=True).numpy()
+    np.testing.assert_allclose(got, ref, rtol=1e-10, atol=1e-13)
+    if base == "linear" and order == M:
+        g = golden("linear_chen.npz")
+        Xg = g["X"]
+        Kg = ar.k_seq(torch.tensor(Xg), None, int(g["num_levels"]), "linear", True, order=int(g["num_levels"]))
+        np.testing.assert_allclose(Kg.numpy(), g["K_chen"], rtol=1e-9, atol=1e-12)
