@@ -77,6 +77,39 @@ GPSIG_DEV float lane_next(float v) { return dpp_f<0x130>(v); }
 GPSIG_DEV float lane_prev(float v) { return dpp_f<0x138>(v); }
 GPSIG_DEV double lane_prev(double v) { return dpp_d<0x138>(v); }
 
+// Reduce-scatter of 4K per-lane values over the 64 lanes of a wave (gfx950 v_permlane32_swap /
+// v_permlane16_swap halve the live values twice, DPP row rotations finish each 16-lane row): on return
+// every lane of row R (lanes 16R .. 16R+15) holds in out[i] the wave total of v[4i + ROW_SLOT[R]].
+// 2K + K swaps and adds plus 4K row steps for 4K totals (a wave-wide scan per value costs 6 steps each).
+constexpr int ROW_SLOT[4] = {0, 2, 1, 3};
+template <int K>
+GPSIG_DEV void wave_reduce_scatter4(const float (&v)[4 * K], float (&out)[K]) {
+  // The swaps are issued as inline asm: ROCm 7.2's __builtin_amdgcn_permlane{16,32}_swap lowering reuses
+  // the first result register for the second (tools/permlane_probe2.hip shows v_add v2, v4, v4 after
+  // v_permlane32_swap v4, v5).  s_nop 1 covers the VALU-write -> permlane-read hazard of the operands.
+  float s1[2 * K];
+#pragma unroll
+  for (int i = 0; i < 2 * K; ++i) {
+    float a = v[2 * i], b = v[2 * i + 1];
+    asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+    s1[i] = a + b;  // lanes < 32: v[2i], lanes >= 32: v[2i+1]
+  }
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    float a = s1[2 * i], b = s1[2 * i + 1];
+    asm volatile("s_nop 1\n\tv_permlane16_swap_b32 %0, %1" : "+v"(a), "+v"(b));
+    out[i] = a + b;
+  }
+#pragma unroll
+  for (int i = 0; i < K; ++i) out[i] += dpp_f<0x128>(out[i]);  // row_ror:8
+#pragma unroll
+  for (int i = 0; i < K; ++i) out[i] += dpp_f<0x124>(out[i]);  // row_ror:4
+#pragma unroll
+  for (int i = 0; i < K; ++i) out[i] += dpp_f<0x122>(out[i]);  // row_ror:2
+#pragma unroll
+  for (int i = 0; i < K; ++i) out[i] += dpp_f<0x121>(out[i]);  // row_ror:1
+}
+
 // Sum over an aligned group of LP lanes, result in every lane of the group.
 template <int LP>
 GPSIG_DEV float group_sum(float v) {

@@ -172,6 +172,11 @@ GPSIG_DEV void wave_sum_last_n(float (&v)[N]) {
 #ifndef GPSIG_BWD_WPE
 #define GPSIG_BWD_WPE 1
 #endif
+// Timing ablations for tools/kbench_vjp.hip only (wrong results): bit 1 drops the per-row x-gradient
+// wave reduction and atomics, bit 2 the inversion scans, bit 4 the adjoint scans.
+#ifndef GPSIG_BWD_ABL
+#define GPSIG_BWD_ABL 0
+#endif
 template <int DP, int W, int LP, int M, int SEED>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_WPE))) void sig_bwd_kernel(BwdArgs p) {
   constexpr int FS = feat_stride(DP);
@@ -182,6 +187,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
   constexpr float L2E = 1.4426950408889634f;
   constexpr int RC = W >= 4 ? 4 : 8;  // rows per chunk of the reverse sweep (<= the forward's anchor period)
   __shared__ __attribute__((aligned(16))) float cbuf[RBF && DIFF ? 4 : 1][RBF && DIFF ? RC : 1][64][2 * W];
+  __shared__ float tbuf[DP <= 8 ? 4 : 1][DP <= 8 ? 4 : 1][DP <= 8 ? DP : 1][64];  // x-gradient row batches
   constexpr int ML = M > 1 ? M - 1 : 1;
   constexpr int CPB = LP * W - 1;  // cells of a column block (the last lane's last column is its halo point)
 
@@ -515,6 +521,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
 
     // point row `pi` of the grid receives dLoss/dk(x_pi, y_j) = Kh[w]: x-gradient reduced over the wave
     // (all pairs of a wave share a), y-gradient accumulated per column
+    // The x-gradient of point row pi is a sum over all 64 lanes (every pair of the wave shares a).  The
+    // reverse sweep emits the point rows in descending order, so for DP <= 8 they are batched by 4: each
+    // lane parks its partials of a row in this wave's LDS slab, and every 4th row one
+    // wave_reduce_scatter4 plus one atomic per channel from 4 lanes serve the batch (a wave-wide scan per
+    // channel and row before: a quarter of the VJP's time at N = 1024, L = 100).
+    constexpr bool BATCH = DP <= 8;
+    int nslot = 0, pi0 = 0;  // rows in the open batch, its first (highest) row
+    auto flush = [&]() {
+      if constexpr (BATCH) {
+        float v[4 * DP], o[DP];
+#pragma unroll
+        for (int k = 0; k < DP; ++k)
+#pragma unroll
+          for (int r = 0; r < 4; ++r) v[4 * k + r] = tbuf[wave][r][k][lane];
+        wave_reduce_scatter4<DP>(v, o);
+        const int R = lane >> 4;
+        const int slot = R == 0 ? 0 : R == 1 ? 2 : R == 2 ? 1 : 3;  // ROW_SLOT
+        if ((lane & 15) == 0 && slot < nslot) {
+#pragma unroll
+          for (int k = 0; k < DP; ++k)
+            if (k < d) unsafeAtomicAdd(gxa + (long long)(pi0 - slot) * d + k, o[k]);
+        }
+        nslot = 0;
+      }
+    };
     auto emit = [&](int pi, const float (&Kh)[W], const float (&kr)[W]) {
       cfloat *xp = fxc + (long long)pi * FS;
       float xi[DP];
@@ -538,12 +569,23 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
 #pragma unroll
         for (int k = 0; k < DP; ++k) B[w][k] = __builtin_fmaf(wg[w], xi[k], B[w][k]);
       }
-      wave_sum_last_n<DP + 1>(s);
-      if (lane == 63) {
+      // this lane's share of dLoss/dx_pi: sum_j wg (y_j - x_pi) (RBF) or sum_j wg y_j (linear)
+      float t[DP];
 #pragma unroll
-        for (int k = 0; k < DP; ++k) {  // compile-time indices (a runtime bound would put s, xi in scratch)
-          const float v = RBF ? __builtin_fmaf(-s[DP], xi[k], s[k]) : s[k];
-          if (k < d) unsafeAtomicAdd(gxa + (long long)pi * d + k, v);
+      for (int k = 0; k < DP; ++k) t[k] = RBF ? __builtin_fmaf(-s[DP], xi[k], s[k]) : s[k];
+      if constexpr (GPSIG_BWD_ABL & 1) {
+        if (t[0] == 1234.5f) gxa[pi] = t[1];  // keep the partials alive
+      } else if constexpr (BATCH) {
+        if (nslot == 0) pi0 = pi;
+#pragma unroll
+        for (int k = 0; k < DP; ++k) tbuf[wave][nslot][k][lane] = t[k];
+        if (++nslot == 4) flush();
+      } else {
+        wave_sum_last_n<DP>(t);
+        if (lane == 63) {
+#pragma unroll
+          for (int k = 0; k < DP; ++k)  // compile-time indices (a runtime bound would put t in scratch)
+            if (k < d) unsafeAtomicAdd(gxa + (long long)pi * d + k, t[k]);
         }
       }
     };
@@ -575,6 +617,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
           float cin[1], tot[1];
           cin[0] = cin_left ? ld_l2(tcar(blk) + (long long)i * ML + s - 1) : 0.0f;
           wave_excl_cols_carry_n<W, 1>(Cm, Sm, cin, tot);
+        } else if constexpr (GPSIG_BWD_ABL & 2) {
+#pragma unroll
+          for (int w = 0; w < W; ++w) Sm[0][w] = Cm[0][w];
         } else {
           group_excl_cols_n<LP, W, 1>(Cm, Sm);  // S_s(i) from the recovered C_s(i)
         }
@@ -605,6 +650,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
 #pragma unroll
             for (int m = 0; m < ML; ++m) ur[m] = uin[m] + tot[m];
           }
+        } else if constexpr (GPSIG_BWD_ABL & 4) {
+#pragma unroll
+          for (int m = 0; m < ML; ++m)
+#pragma unroll
+            for (int w = 0; w < W; ++w) r[m][w] = v[m][w];
         } else {
           group_rexcl_cols_n<LP, W, ML>(v, r);
         }
@@ -738,6 +788,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
       for (int w = 0; w < W; ++w) Kh[w] = -Ep[w];
       emit(0, Kh, kr1);
     }
+    if (nslot > 0) flush();  // the last, partial batch
 
     // ---- y-gradient of the block's points
     if (pair_ok) {

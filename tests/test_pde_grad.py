@@ -78,3 +78,39 @@ def test_pde_cross_vjp_matches_adjoint(n):
             ry[b] += G[a, b] * gy
     assert norm_rel_err(gX.cpu().numpy(), rx) < 1e-5
     assert norm_rel_err(gY.cpu().numpy(), ry) < 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("L,n", [(100, 1), (200, 1), (129, 2), (300, 1)])
+def test_pde_kdiag_vjp_wide_grids(L, n):
+    """Wide grids of the adjoint kernel: 2^n (L-1) = 198 (W = 4, step-ordered K_rev cells), 398 and 512
+    (W = 8) and 598 refined columns (W = 16, row-major K_rev cells with the reversed read)."""
+    from gpsig_amd import ops
+    rng = np.random.default_rng(L + n)
+    X = np.cumsum(rng.standard_normal((3, L, 3)), 1) / np.sqrt(L * 3) * 2
+    w = rng.standard_normal(3)
+    K, Kr = pde.pde_diag_grids(X, n, 1)
+    ref = pde_grad.kdiag_grad(X, np.tril(K), np.tril(Kr), n) * w[:, None, None]
+    got = ops.pde_diag_vjp(torch.tensor(X, device=DEV), torch.tensor(w, device=DEV), n, 1)
+    assert norm_rel_err(got.cpu().numpy(), ref) < 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("l2,n", [(300, 0), (700, 0), (130, 1)])
+def test_pde_cross_vjp_wide_grids(l2, n):
+    """Cross pairs whose refined column count J = 2^n (l2 - 1) is 299 / 258 (W = 8) and 699 (W = 16)."""
+    from gpsig_amd import ops
+    rng = np.random.default_rng(l2)
+    X = np.cumsum(rng.standard_normal((2, 12, 2)), 1) * 0.3
+    Y = np.cumsum(rng.standard_normal((2, l2, 2)), 1) * 0.3 / np.sqrt(l2 / 10)
+    G = rng.standard_normal((2, 2))
+    gX, gY = ops.pde_gram_vjp(torch.tensor(X, device=DEV), torch.tensor(Y, device=DEV),
+                              torch.tensor(G, device=DEV), n, 1)
+    rx, ry = np.zeros_like(X), np.zeros_like(Y)
+    for a in range(2):
+        for b in range(2):
+            gx, gy = pde_grad.pair_grad(X[a], Y[b], n, 1)
+            rx[a] += G[a, b] * gx
+            ry[b] += G[a, b] * gy
+    assert norm_rel_err(gX.cpu().numpy(), rx) < 1e-5
+    assert norm_rel_err(gY.cpu().numpy(), ry) < 1e-5
