@@ -1,0 +1,367 @@
+// gpsig_amd -- gradient of the Goursat-PDE signature kernel on gfx950.
+//
+// The reference's only hand-written gradient is for the PDE kernel (kernels_pde.py:465-509,
+// _KdiagGrad, over the grids K and K_rev returned by sigKer_fast.pyx:15-62; the same formula for the
+// CUDA op in covariance_op/_untrunc_cov_grad.py:25-77):
+//   KK[s, t] = K[s, t] * K_rev_rev[s+1, t+1],   K_rev_rev = K_rev flipped in both axes,
+//   K_rev    = the solution on the time-reversed paths with the first-order scheme (solver 0),
+//   G[i]     = 4^-n sum_{s in coarse row i} sum_t KK[s, t] dy_{t >> n}
+//   dK/dx_i  = G[i-1] - G[i]   (times 2 for k(x, x), times the upstream gradient of K[-1, -1]).
+// For a cross pair (x, y) the same adjoint gives dK/dy_j from the column sums.
+//
+// One wave per pair, the coarse-row skewed sweep of pde.hip (pde_rep_kernel: lane l owns W fine
+// columns = W/REP coarse columns, one step = one coarse row of REP = 2^n fine rows), fp64 solution as
+// the reference, and nothing grid-sized in memory:
+//   * R(i, c) := K_rev[I-i][J-c] solves the same scheme from the corner (I, J) towards (0, 0)
+//     (R(p, q) = R(p+1, q) + R(p, q+1) + R(p+1, q+1) (inc(p, q) - 1), solver 0), so KK[i][c] =
+//     K(i, c) R(i+1, c+1).  Swept with the mirrored skew (lane l takes its right boundary from lane
+//     l+1; coarse row ic at R step IC + U - 2 - ic - l, U = lanes used), lane l meets coarse row ic at
+//     the R step IC + U - 2 - s where s = ic + l is the forward step of the same row: walking the
+//     forward steps backwards visits, in every lane, exactly the cells the R sweep needs.
+//   * pass A sweeps K forward and stores its front (the lane's last fine row, W values, plus the
+//     REP - 1 other right-column values and the corner it hands on) every H steps to the workspace;
+//   * pass B walks the chunks of H steps backwards: restore the chunk's front, re-run its H forward
+//     steps keeping the K corner of every fine cell in registers, then run H steps of the R sweep,
+//     which consume them in reverse.  The fronts and the kept corners are fp32: they enter only the
+//     products KK (relative error ~1e-7 on the gradient), never the fp64 recurrences of the R sweep.
+//   * per coarse cell the REP x REP products are summed first; the increments are constant over it,
+//     so the row (dK/dx) and column (dK/dy) contractions cost 2 DP FMAs per coarse cell.  Row partials
+//     go to the wave's LDS row accumulators (ds_add_f64; lanes hold distinct coarse rows at a step),
+//     column partials stay in registers.
+// Three sweeps of the grid instead of the previous two sweeps plus an fp64 K_rev grid stored and
+// re-read through HBM (~0.3 MB per pair at L = 100, dyadic 1).
+#pragma once
+#include "sig_common.h"
+
+namespace gpsig {
+
+struct PdeBwdArgs {
+  const float *X, *Y;
+  int n1, l1, n2, l2, d;
+  int dyadic, solver;
+  int pair_mode, row_begin, row_end;
+  int ntb, tiles_a0;
+  const float *gout;  // DIAG: (n1,); RECT: (n1, n2)
+  float *gX, *gY;     // accumulated (n1, l1, d), (n2, l2, d)
+  float *fronts;      // workspace: per evaluated pair, nfronts x (W + REP) x 64 floats (pde_front_floats)
+};
+
+GPSIG_DEV double lane_next_d(double v) { return dpp_d<0x130>(v); }
+
+// coarse steps per stored front: the chunk's K corners (H x REP x W floats per lane) live in registers
+template <int W, int REP>
+constexpr int pde_chunk() { return REP * W >= 32 ? 1 : 32 / (REP * W); }
+
+// Columns per lane of the adjoint kernel: the smallest power of two >= REP with ceil(J / W) <= 64 lanes
+// (J <= 1024 fine columns); 0 when unsupported.
+__host__ __device__ inline int pde_bwd_cols(int J, int rep) {
+  for (int W = 1; W <= 16; W *= 2)
+    if (W >= rep && (long long)64 * W >= J) return (rep * W <= 64) ? W : 0;
+  return 0;
+}
+// fp32 words of the stored K fronts of one pair
+inline long long pde_front_floats(int l1, int l2, int dyadic) {
+  if (dyadic < 0 || dyadic > 4) return 0;
+  const int rep = 1 << dyadic;
+  const long long JL = (long long)(l2 - 1) * rep;
+  if (JL > 1024) return 0;
+  const int J = (int)JL, W = pde_bwd_cols(J, rep);
+  if (W == 0) return 0;
+  const long long H = rep * W >= 32 ? 1 : 32 / (rep * W), U = (J + W - 1) / W;
+  const long long nfr = ((l1 - 1) + U - 1 + H - 1) / H;
+  return nfr * (W + rep) * 64;
+}
+
+template <int DP, int W, int REP, bool COLS>
+__global__ __launch_bounds__(256) void pde_adj_kernel(PdeBwdArgs p) {
+  static_assert(W % REP == 0, "a lane owns whole coarse columns");
+  constexpr int WC = W / REP;
+  constexpr int H = pde_chunk<W, REP>();
+  constexpr int FW = W + REP;  // front words per lane: up[W], last[0 .. REP-2], corner_prev
+  extern __shared__ __attribute__((aligned(16))) double ldsd[];
+  const int lane = threadIdx.x & 63;
+  const int wave = wave_uniform(threadIdx.x >> 6);
+  const bool diag = p.pair_mode == GPSIG_PAIRS_DIAG;
+  int a, b;
+  if (diag) {
+    a = p.row_begin + (int)blockIdx.x * 4 + wave;
+    b = a;
+  } else {
+    a = (p.tiles_a0 + (int)blockIdx.x / p.ntb) * 4 + wave;
+    b = (int)blockIdx.x % p.ntb;
+  }
+  const bool ok = a >= p.row_begin && a < p.row_end && b < p.n2;  // wave-uniform
+  if (!ok) { a = p.row_begin; b = diag ? a : 0; }
+
+  const double inv_factor = 1.0 / (double)(REP * REP);
+  const int IC = p.l1 - 1, JC = p.l2 - 1;
+  const int J = JC * REP;
+  const int d = p.d;
+  const float *x = p.X + (long long)a * p.l1 * d;
+  const float *y = p.Y + (long long)b * p.l2 * d;
+  const long long pidx = diag ? (long long)(a - p.row_begin) : (long long)(a - p.row_begin) * p.n2 + b;
+  const int U = (J + W - 1) / W;
+  const int nsteps = IC + U - 1;
+  const int nfr = (nsteps + H - 1) / H;
+  float *__restrict__ fr = p.fronts + pidx * (long long)nfr * FW * 64;
+
+  // LDS: [wave] { dx (IC x DP floats, as doubles' storage) | coarse-row accumulators (IC x DP doubles) }
+  double *wl = ldsd + (size_t)wave * IC * DP * 2;
+  float *dxs = reinterpret_cast<float *>(wl);
+  double *gacc = wl + (size_t)IC * DP;
+  for (int r = lane; r < IC; r += 64) {
+#pragma unroll
+    for (int k = 0; k < DP; ++k) {
+      dxs[r * DP + k] = k < d ? x[(r + 1) * d + k] - x[r * d + k] : 0.0f;
+      gacc[r * DP + k] = 0.0;
+    }
+  }
+  // y increments of this lane's coarse columns
+  float dy[WC][DP];
+#pragma unroll
+  for (int w = 0; w < WC; ++w) {
+    int cj = lane * WC + w;
+    cj = cj < JC - 1 ? cj : JC - 1;
+#pragma unroll
+    for (int k = 0; k < DP; ++k) dy[w][k] = k < d ? y[(cj + 1) * d + k] - y[cj * d + k] : 0.0f;
+  }
+  __syncthreads();
+
+  const bool s1 = p.solver == 1;
+  const bool hybrid = diag && p.solver == 0;
+  auto incs = [&](int ci, double (&inc)[WC], float (&dxv)[DP]) {
+    const float *dxr = dxs + ci * DP;
+#pragma unroll
+    for (int k = 0; k < DP; ++k) dxv[k] = dxr[k];
+#pragma unroll
+    for (int w = 0; w < WC; ++w) {
+      float incf = 0.0f;
+#pragma unroll
+      for (int k = 0; k < DP; ++k) incf = __builtin_fmaf(dxv[k], dy[w][k], incf);
+      inc[w] = (double)incf * inv_factor;
+    }
+  };
+
+  // ---- K sweep state and one forward step (pde_rep_kernel's scheme); kc[r][w] = K(i, c) of cell (i, c)
+  double up[W], last[REP], corner_prev;
+  auto kstep = [&](int s, float (&kc)[REP][W]) {
+    double left[REP];
+#pragma unroll
+    for (int r = 0; r < REP; ++r) {
+      left[r] = lane_prev(last[r]);
+      if (lane == 0) left[r] = 1.0;
+    }
+    const int ci = s - lane;
+    if (ci >= 0 && ci < IC && lane < U) {
+      double inc[WC], A[WC], B[WC];
+      float dxv[DP];
+      incs(ci, inc, dxv);
+#pragma unroll
+      for (int w = 0; w < WC; ++w) {
+        const double inc2 = inc[w] * inc[w];
+        A[w] = s1 ? 1.0 + 0.5 * inc[w] + (1.0 / 12) * inc2 : inc[w];
+        B[w] = s1 ? 1.0 - (1.0 / 12) * inc2 : inc[w] - 1.0;
+      }
+#pragma unroll
+      for (int r = 0; r < REP; ++r) {
+        const int i = ci * REP + r;
+        double lft = left[r];
+        double cor = r == 0 ? corner_prev : left[r - 1];
+        // columns c >= J are updated too (as pde_rep_kernel): they never reach a real cell
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          const double upw = up[w];
+          double kn;
+          if (s1) {
+            kn = (upw + lft) * A[w / REP] - cor * B[w / REP];
+          } else {
+            kn = (upw + lft) + cor * B[w / REP];
+            if (hybrid && lane * W + w == i) {
+              const double t = A[w / REP], t2 = t * t;
+              kn = (upw + lft) * (1.0 + 0.5 * t + (1.0 / 12) * t2) - cor * (1.0 - (1.0 / 12) * t2);
+            }
+          }
+          kc[r][w] = (float)cor;
+          cor = upw;
+          lft = kn;
+          up[w] = kn;
+        }
+        last[r] = lft;
+      }
+    }
+    corner_prev = left[REP - 1];
+  };
+
+  // ---- pass A: K forward, a front every H steps (last[REP-1] is up[W-1] after any step)
+#pragma unroll
+  for (int w = 0; w < W; ++w) up[w] = 1.0;
+#pragma unroll
+  for (int r = 0; r < REP; ++r) last[r] = 1.0;
+  corner_prev = 1.0;
+  const int nst = ok ? nsteps : 0;  // invalid waves still reach the barrier below
+  for (int s0 = 0; s0 < nst; s0 += H) {
+    float *f = fr + (long long)(s0 / H) * FW * 64;
+#pragma unroll
+    for (int w = 0; w < W; ++w) f[w * 64 + lane] = (float)up[w];
+#pragma unroll
+    for (int r = 0; r + 1 < REP; ++r) f[(W + r) * 64 + lane] = (float)last[r];
+    f[(W + REP - 1) * 64 + lane] = (float)corner_prev;
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      float kc[REP][W];
+      if (s0 + h < nsteps) kstep(s0 + h, kc);
+    }
+  }
+
+  // ---- pass B: chunks backwards; the R sweep runs continuously in its own step order
+  double ru[W], rlast[REP], rcorner = 1.0;
+  double gcol[WC][DP];
+#pragma unroll
+  for (int w = 0; w < W; ++w) ru[w] = 1.0;
+#pragma unroll
+  for (int r = 0; r < REP; ++r) rlast[r] = 1.0;
+#pragma unroll
+  for (int w = 0; w < WC; ++w)
+#pragma unroll
+    for (int k = 0; k < DP; ++k) gcol[w][k] = 0.0;
+  for (int s0 = ((nst - 1) / H) * H; nst > 0 && s0 >= 0; s0 -= H) {
+    const float *f = fr + (long long)(s0 / H) * FW * 64;
+#pragma unroll
+    for (int w = 0; w < W; ++w) up[w] = (double)f[w * 64 + lane];
+#pragma unroll
+    for (int r = 0; r + 1 < REP; ++r) last[r] = (double)f[(W + r) * 64 + lane];
+    last[REP - 1] = up[W - 1];
+    corner_prev = (double)f[(W + REP - 1) * 64 + lane];
+    float kc[H][REP][W];
+#pragma unroll
+    for (int h = 0; h < H; ++h)
+      if (s0 + h < nsteps) kstep(s0 + h, kc[h]);
+#pragma unroll
+    for (int h = H - 1; h >= 0; --h) {
+      if (s0 + h >= nsteps) continue;
+      double right[REP];
+#pragma unroll
+      for (int r = 0; r < REP; ++r) {
+        right[r] = lane_next_d(rlast[r]);
+        if (lane == 63) right[r] = 1.0;
+      }
+      const int ci = s0 + h - lane;
+      if (ci >= 0 && ci < IC && lane < U) {
+        double inc[WC], S[WC];
+        float dxv[DP];
+        incs(ci, inc, dxv);
+#pragma unroll
+        for (int w = 0; w < WC; ++w) {
+          inc[w] -= 1.0;
+          S[w] = 0.0;
+        }
+#pragma unroll
+        for (int r = REP - 1; r >= 0; --r) {
+          double rgt = right[r];
+          double cor = r == REP - 1 ? rcorner : right[r + 1];
+#pragma unroll
+          for (int w = W - 1; w >= 0; --w) {
+            const int c = lane * W + w;
+            const double upw = ru[w];
+            const double rn = (upw + rgt) + cor * inc[w / REP];
+            if (c < J) {  // columns >= J keep the boundary value 1
+              // KK[i][c] = K(i, c) * R(i+1, c+1) = K[i][c] * K_rev[I-1-i][J-1-c]
+              S[w / REP] = __builtin_fma((double)kc[h][r][w], cor, S[w / REP]);
+              cor = upw;
+              rgt = rn;
+              ru[w] = rn;
+            }
+          }
+          rlast[r] = rgt;
+        }
+        double grow[DP];
+#pragma unroll
+        for (int k = 0; k < DP; ++k) grow[k] = 0.0;
+#pragma unroll
+        for (int w = 0; w < WC; ++w)
+#pragma unroll
+          for (int k = 0; k < DP; ++k) {
+            grow[k] = __builtin_fma(S[w], (double)dy[w][k], grow[k]);
+            if constexpr (COLS) gcol[w][k] = __builtin_fma(S[w], (double)dxv[k], gcol[w][k]);
+          }
+#pragma unroll
+        for (int k = 0; k < DP; ++k)
+          if (k < d) atomicAdd(gacc + ci * DP + k, grow[k]);
+      }
+      rcorner = right[0];
+    }
+  }
+  __syncthreads();  // the row accumulators are complete
+  if (!ok) return;
+
+  // dK/dx_i = G[i-1] - G[i] with G[r] = 4^-n gacc[r] (x2 for k(x, x)), times the upstream gradient
+  const float g = diag ? p.gout[a] : p.gout[(long long)a * p.n2 + b];
+  const double sx = (diag ? 2.0 : 1.0) * inv_factor * (double)g;
+  float *gxa = p.gX + (long long)a * p.l1 * d;
+  for (int r = lane; r <= IC; r += 64)
+    for (int k = 0; k < d; ++k) {
+      const double gp = r > 0 ? gacc[(r - 1) * DP + k] : 0.0;
+      const double gc = r < IC ? gacc[r * DP + k] : 0.0;
+      unsafeAtomicAdd(gxa + (long long)r * d + k, (float)(sx * (gp - gc)));
+    }
+  if (diag || !COLS) return;
+  // columns: H[j] = 4^-n sum over coarse column j; dK/dy_j = H[j-1] - H[j]
+  const double sy = inv_factor * (double)g;
+  float *gyb = p.gY + (long long)b * p.l2 * d;
+#pragma unroll
+  for (int w = 0; w < WC; ++w) {
+    const int jc = lane * WC + w;
+    if (jc >= JC) continue;
+#pragma unroll
+    for (int k = 0; k < DP; ++k) {  // compile-time indices: a runtime bound would put gcol in scratch
+      if (k >= d) continue;
+      const float v = (float)(sy * gcol[w][k]);
+      unsafeAtomicAdd(gyb + (long long)(jc + 1) * d + k, v);
+      unsafeAtomicAdd(gyb + (long long)jc * d + k, -v);
+    }
+  }
+}
+
+template <int DP, int W, int REP>
+static int launch_pde_adj(const PdeBwdArgs &a, long long nblocks, hipStream_t s) {
+  if constexpr (W < REP || REP * W > 64) {
+    return GPSIG_EUNSUPPORTED;
+  } else {
+    const size_t lds = (size_t)4 * (a.l1 - 1) * DP * 2 * sizeof(double);
+    if (lds > 160 * 1024) return GPSIG_EUNSUPPORTED;
+    // the column (dK/dy) accumulators only for cross pairs; k(x, x) takes twice the row part
+    if (a.pair_mode == GPSIG_PAIRS_DIAG)
+      hipLaunchKernelGGL((pde_adj_kernel<DP, W, REP, false>), dim3((unsigned)nblocks), dim3(256), lds, s, a);
+    else
+      hipLaunchKernelGGL((pde_adj_kernel<DP, W, REP, true>), dim3((unsigned)nblocks), dim3(256), lds, s, a);
+    return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
+  }
+}
+
+template <int DP, int REP>
+static int pde_adj_w(const PdeBwdArgs &a, long long nblocks, int W, hipStream_t s) {
+  switch (W) {
+    case 1: return launch_pde_adj<DP, 1, REP>(a, nblocks, s);
+    case 2: return launch_pde_adj<DP, 2, REP>(a, nblocks, s);
+    case 4: return launch_pde_adj<DP, 4, REP>(a, nblocks, s);
+    case 8: return launch_pde_adj<DP, 8, REP>(a, nblocks, s);
+    case 16: return launch_pde_adj<DP, 16, REP>(a, nblocks, s);
+    default: return GPSIG_EUNSUPPORTED;
+  }
+}
+
+// one channel count (pde_bwd_inst.hip, one unit per DP)
+template <int DP>
+int pde_bwd_launch_dp(const PdeBwdArgs &a, long long nblocks, hipStream_t s) {
+  const int rep = 1 << a.dyadic;
+  const int W = pde_bwd_cols(rep * (a.l2 - 1), rep);
+  switch (a.dyadic) {
+    case 0: return pde_adj_w<DP, 1>(a, nblocks, W, s);
+    case 1: return pde_adj_w<DP, 2>(a, nblocks, W, s);
+    case 2: return pde_adj_w<DP, 4>(a, nblocks, W, s);
+    case 3: return pde_adj_w<DP, 8>(a, nblocks, W, s);
+    default: return GPSIG_EUNSUPPORTED;
+  }
+}
+
+}  // namespace gpsig

@@ -83,7 +83,10 @@ def test_vjp_and_feature_entry_points_validate_arguments():
     assert lib.gpsig_signature(None, 4, 10, 3, 3, None, None) == L.GPSIG_EINVAL
     assert lib.gpsig_signature_vjp(None, 4, 10, 3, 3, None, None, None) == L.GPSIG_EINVAL
     assert lib.gpsig_signature_channels(5, 3) == 5 + 25 + 125
-    assert lib.gpsig_pde_vjp_workspace_bytes(2, 10, 10, 1) == 2 * (18 + 18 - 1) * 18 * 8  # W = 1: 18 lanes
+    # J = 18 fine columns at dyadic 1: W = 2 per lane, U = 9 lanes, 9 + 9 - 1 = 17 coarse steps, a front every
+    # 32 / (2 * 2) = 8 steps -> 3 fronts of (W + REP) x 64 floats per pair
+    assert lib.gpsig_pde_vjp_workspace_bytes(2, 10, 10, 1) == 2 * 3 * (2 + 2) * 64 * 4
+    assert lib.gpsig_pde_vjp_workspace_bytes(2, 10, 1100, 0) == 0  # J > 1024: unsupported
 
 
 def test_graph_capture_refuses_host_tensors_and_kernel_to():
