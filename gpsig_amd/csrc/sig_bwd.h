@@ -26,6 +26,10 @@
 
 namespace gpsig {
 
+// dLoss/dscale is accumulated into this many partial sums (workspace) and reduced after the launch: one
+// address per level for every wave of the grid serialised the atomics (+7.7 ms at N = 1024, L = 100).
+constexpr int GSCALE_SLOTS = 64;
+
 struct BwdArgs {
   const float *FX, *FY;  // feature records (n1,l1,FS), (n2,l2,FS)
   int n1, l1, n2, l2, d;
@@ -39,7 +43,8 @@ struct BwdArgs {
   long long g_ld, g_lvl;
   const float *rs1, *rs2, *scale;
   float jitter;
-  float *gX, *gY, *grs1, *grs2, *gscale;
+  float *gX, *gY, *grs1, *grs2;
+  float *gscale;  // GSCALE_SLOTS x (M + 1) partial sums (workspace), see gpsig_sig_gram_vjp
   const float *state;  // optional saved forward state (RECT / UPPER), see gpsig_sig_gram_state
   // column blocks (LP = 64, sequences longer than one lane group covers): per-pair scratch of
   // scr_stride floats at scratch + (blockIdx.x * 4 + wave) * scr_stride, see bwd_scratch_floats
@@ -429,48 +434,73 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
 
   // ---- per-level weights g_m = dLoss/dK_m(a, b) and the normalisation / scale terms
 
-  float gw[M + 1];
-  {
-    const bool upper_off = p.pair_mode == GPSIG_PAIRS_UPPER && a != bl;
-    const float jit = (p.pair_mode == GPSIG_PAIRS_UPPER && a == bl) ? p.jitter : 0.0f;
+  // per-level weights g_m = dLoss/dK_m(a, b) and the normalisation / scale factors of this pair
+  const bool upper_off = p.pair_mode == GPSIG_PAIRS_UPPER && a != bl;
+  const float jit = (p.pair_mode == GPSIG_PAIRS_UPPER && a == bl) ? p.jitter : 0.0f;
+  auto pair_terms = [&](float (&gs)[M + 1], float (&sc)[M + 1], float (&r1)[M + 1], float (&r2)[M + 1]) {
     float gsum = 0.0f;
     if (!diag && !p.gout_levels) {
       gsum = p.gout[(long long)a * p.g_ld + bl];
       if (upper_off) gsum += p.gout[(long long)bl * p.g_ld + a];
     }
-    float gsc[M + 1];
 #pragma unroll
     for (int m = 0; m <= M; ++m) {
-      float gs;
+      float g;
       if (diag) {
-        gs = p.gout[(long long)m * p.g_lvl + a];
+        g = p.gout[(long long)m * p.g_lvl + a];
       } else if (p.gout_levels) {
-        gs = p.gout[(long long)m * p.g_lvl + (long long)a * p.g_ld + bl];
-        if (upper_off) gs += p.gout[(long long)m * p.g_lvl + (long long)bl * p.g_ld + a];
+        g = p.gout[(long long)m * p.g_lvl + (long long)a * p.g_ld + bl];
+        if (upper_off) g += p.gout[(long long)m * p.g_lvl + (long long)bl * p.g_ld + a];
       } else {
-        gs = gsum;
+        g = gsum;
       }
-      if (!pair_ok) gs = 0.0f;
-      const float sc = p.scale ? p.scale[m] : 1.0f;
-      const float r1 = p.rs1 ? p.rs1[(long long)m * p.n1 + a] : 1.0f;
-      const float r2 = p.rs2 ? p.rs2[(long long)m * p.n2 + bl] : 1.0f;
-      gw[m] = gs * sc * r1 * r2;
-      gsc[m] = gs * (K[m] + jit) * r1 * r2;  // dLoss/dscale_m contribution
-      if (p.rs1 && gl == 0 && pair_ok && !diag) {
-        const float t = gs * sc * (K[m] + jit);
-        if (p.grs1) unsafeAtomicAdd(p.grs1 + (long long)m * p.n1 + a, t * r2);
-        if (p.grs2) unsafeAtomicAdd(p.grs2 + (long long)m * p.n2 + bl, t * r1);
-      }
+      gs[m] = pair_ok ? g : 0.0f;
+      sc[m] = p.scale ? p.scale[m] : 1.0f;
+      r1[m] = p.rs1 ? p.rs1[(long long)m * p.n1 + a] : 1.0f;
+      r2[m] = p.rs2 ? p.rs2[(long long)m * p.n2 + bl] : 1.0f;
     }
-    if (p.gscale && !diag) {
-      // one pair per lane group: keep the group leader's value, then reduce over the wave
+  };
+  float gw[M + 1];
+  {
+    float gs[M + 1], sc[M + 1], r1[M + 1], r2[M + 1];
+    pair_terms(gs, sc, r1, r2);
 #pragma unroll
-      for (int m = 0; m <= M; ++m) gsc[m] = (gl == 0) ? gsc[m] : 0.0f;
-      wave_sum_last_n<M + 1>(gsc);
-      if (lane == 63)
-        for (int m = 0; m <= M; ++m) unsafeAtomicAdd(p.gscale + m, gsc[m]);
-    }
+    for (int m = 0; m <= M; ++m) gw[m] = gs[m] * sc[m] * r1[m] * r2[m];
   }
+  // dLoss/drs and dLoss/dscale of this pair, added after the sweep (their atomics would otherwise sit in
+  // vmcnt ahead of every load of the sweep; the factors are reloaded there, only K stays live):
+  // grs1[m, a] summed over the wave (its pairs all share a), grs2[m, b] per pair, gscale into one of
+  // GSCALE_SLOTS partial sums (summed over the wave)
+  auto norm_terms = [&]() {
+    if (diag || !(p.gscale || (p.rs1 && (p.grs1 || p.grs2)))) return;
+    float gs[M + 1], sc[M + 1], r1[M + 1], r2[M + 1];
+    pair_terms(gs, sc, r1, r2);
+    const bool lead = gl == 0 && pair_ok;  // one contribution per pair
+    float g1[M + 1], g2[M + 1], gsc[M + 1];
+#pragma unroll
+    for (int m = 0; m <= M; ++m) {
+      const float t = gs[m] * sc[m] * (K[m] + jit);
+      g1[m] = lead ? t * r2[m] : 0.0f;
+      g2[m] = t * r1[m];
+      gsc[m] = lead ? gs[m] * (K[m] + jit) * r1[m] * r2[m] : 0.0f;
+    }
+    if (p.rs1 && p.grs1) {
+      wave_sum_last_n<M + 1>(g1);
+      if (lane == 63)
+        for (int m = 0; m <= M; ++m) unsafeAtomicAdd(p.grs1 + (long long)m * p.n1 + a, g1[m]);
+    }
+    if (p.rs1 && p.grs2 && lead) {
+#pragma unroll
+      for (int m = 0; m <= M; ++m) unsafeAtomicAdd(p.grs2 + (long long)m * p.n2 + bl, g2[m]);
+    }
+    if (p.gscale) {
+      wave_sum_last_n<M + 1>(gsc);
+      if (lane == 63) {
+        float *slot = p.gscale + (long long)(lblk & (GSCALE_SLOTS - 1)) * (M + 1);
+        for (int m = 0; m <= M; ++m) unsafeAtomicAdd(slot + m, gsc[m]);
+      }
+    }
+  };
 
   // ---- reverse sweep, blocks right to left
   float *__restrict__ gxa = p.gX + (long long)a * l1 * p.d;
@@ -805,6 +835,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
       }
     }
   }
+  norm_terms();
 }
 
 // Column geometry of the backward kernel: W columns per lane, LP lanes per pair.  The lane keeps

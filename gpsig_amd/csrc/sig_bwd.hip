@@ -32,6 +32,16 @@ static int bwd_pad(int d) {
 }
 
 static size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
+static constexpr size_t GSC_BYTES = GSCALE_SLOTS * 9 * sizeof(float);  // dscale partials (M <= 8)
+
+// gscale[m] += sum of the GSCALE_SLOTS partial sums of level m
+__global__ void gscale_reduce_kernel(const float *__restrict__ slots, int levels, float *__restrict__ gscale) {
+  const int m = threadIdx.x;
+  if (m >= levels) return;
+  float s = 0.0f;
+  for (int k = 0; k < GSCALE_SLOTS; ++k) s += slots[k * levels + m];
+  gscale[m] += s;
+}
 static inline long long upper_prefix(long long r, long long ntb, long long k) { return r * ntb - k * r * (r - 1) / 2; }
 
 }  // namespace gpsig
@@ -68,7 +78,8 @@ extern "C" int gpsig_sig_gram_vjp(const float *X, int n1, int l1, const float *Y
   const size_t fx_b = align256((size_t)n1 * l1 * feat_stride(DP) * sizeof(float));
   const size_t fy_b = same ? 0 : align256((size_t)n2 * l2 * feat_stride(DP) * sizeof(float));
   const size_t scr_b = (size_t)scr_stride * 4 * BWD_CHUNK_BLOCKS * sizeof(float);
-  if (!workspace || workspace_bytes < fx_b + fy_b + scr_b) return GPSIG_EWORKSPACE;
+  if (!workspace || workspace_bytes < fx_b + fy_b + scr_b + GSC_BYTES) return GPSIG_EWORKSPACE;
+  float *gsc_slots = reinterpret_cast<float *>(static_cast<char *>(workspace) + fx_b + fy_b + scr_b);
   float *FX = static_cast<float *>(workspace);
   float *FY = same ? FX : reinterpret_cast<float *>(static_cast<char *>(workspace) + fx_b);
   int rc = features(X, n1, l1, d, DP, FX, s);
@@ -93,7 +104,11 @@ extern "C" int gpsig_sig_gram_vjp(const float *X, int n1, int l1, const float *Y
   a.gY = pair_mode == GPSIG_PAIRS_RECT ? gY : gX;
   a.grs1 = grs1;
   a.grs2 = pair_mode == GPSIG_PAIRS_RECT ? grs2 : grs1;
-  a.gscale = gscale;
+  a.gscale = nullptr;
+  if (gscale && pair_mode != GPSIG_PAIRS_DIAG) {
+    if (hipMemsetAsync(gsc_slots, 0, GSC_BYTES, s) != hipSuccess) return GPSIG_ELAUNCH;
+    a.gscale = gsc_slots;
+  }
   a.state = state;
   a.nblk = nblk;
   a.scratch = scr_stride ? reinterpret_cast<float *>(static_cast<char *>(workspace) + fx_b + fy_b) : nullptr;
@@ -132,6 +147,10 @@ extern "C" int gpsig_sig_gram_vjp(const float *X, int n1, int l1, const float *Y
     }
     if (rc) return rc;
   }
+  if (a.gscale) {
+    hipLaunchKernelGGL(gscale_reduce_kernel, dim3(1), dim3(64), 0, s, gsc_slots, num_levels + 1, gscale);
+    if (hipGetLastError() != hipSuccess) return GPSIG_ELAUNCH;
+  }
   return GPSIG_OK;
 }
 
@@ -142,5 +161,6 @@ extern "C" size_t gpsig_sig_vjp_workspace_bytes(int n1, int l1, int n2, int l2, 
   const int nblk = bwd_blocks(l2, difference != 0, geo);
   const long long scr = bwd_scratch_floats(difference ? l1 - 1 : l1, num_levels, geo.W, nblk);
   return align256((size_t)n1 * l1 * feat_stride(DP) * sizeof(float)) +
-         align256((size_t)n2 * l2 * feat_stride(DP) * sizeof(float)) + (size_t)scr * 4 * BWD_CHUNK_BLOCKS * sizeof(float);
+         align256((size_t)n2 * l2 * feat_stride(DP) * sizeof(float)) + (size_t)scr * 4 * BWD_CHUNK_BLOCKS * sizeof(float) +
+         GSC_BYTES;
 }
