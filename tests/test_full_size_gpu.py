@@ -90,3 +90,39 @@ def test_kuf_full_size_C4(increments):
                             return_levels=True, increments=increments)
     got = K[:, torch.as_tensor(Ts, device=DEV)][:, :, St].cpu().numpy()
     assert (norm_rel_err(got[1:], exp[1:], axis_levels=True) < TOL).all()
+
+
+def test_vosf_kuf_full_size_C4():
+    """The VOSF reading of C4 (BASELINE.json configs[3], inducing_variables_vosf.py:212-269): Kuf of
+    Mz = 512 orthogonal signature features against N = 4096 sequences, L = 100, D = 5 (signature level
+    4, the first 511 coordinates, computed on the device and scaled per level), the normalised kernel
+    (Kuf divided by the per-level K_norms of each sequence).  Column subset = the call on the subset;
+    a subsample against exact Chen signatures (oracle/chen.py) and the float64 oracle's diagonal."""
+    import gpsig_amd
+    from gpsig_amd import inducing_variables_vosf as iv
+    from gpsig_amd import signatures as sg
+    from oracle import chen
+    Mz, N, L, D, lev = 512, 4096, 100, 5, 5
+    X = walks(N, L, D)
+    Xt = torch.as_tensor(X.reshape(N, -1), device=DEV)
+    var = np.linspace(0.5, 1.5, lev + 1)
+    k = gpsig_amd.SignatureLinear(L * D, D, lev, order=lev, variances=var)
+    feat = iv.TruncInducingOrthogonalTensors(L * D, D, Mz, compute_sig=True)
+    Kzz, Kzx, Kxx = feat.Kuu_Kuf_Kff(k, Xt)
+    assert Kzz.shape == (Mz, Mz) and Kzx.shape == (Mz, N) and Kxx.shape == (N,)
+    torch.testing.assert_close(Kxx, torch.full((N,), float(var.sum()), device=DEV, dtype=Kxx.dtype))
+    S = np.unique(np.linspace(0, N - 1, 12).astype(int))
+    St = torch.as_tensor(S, device=DEV)
+    _, Kzx_s, _ = feat.Kuu_Kuf_Kff(k, Xt[St])
+    torch.testing.assert_close(Kzx[:, St], Kzx_s, rtol=0, atol=0)
+    slv = sg.compute_trunc(Mz, D)
+    assert slv == 4
+    Xs = X[S].astype(np.float64)
+    sig = [chen.signature(x, slv) for x in Xs]
+    ref = np.stack([np.concatenate([[1.0]] + s[1:]) for s in sig])[:, :Mz].T  # (Mz, |S|)
+    reps = np.repeat(np.arange(slv + 1), [D ** i for i in range(slv + 1)])[:Mz]
+    # normalised kernel: level m of k(x, x) is |S_m(x)|^2 (the exact signature kernel, order = num_levels)
+    knorm = np.stack([[1.0] + [float(np.dot(s[m], s[m])) for m in range(1, slv + 1)] for s in
+                      [chen.signature(x, lev) for x in Xs]]).T  # (slv + 1, |S|)
+    ref = ref * np.sqrt(var[reps])[:, None] / np.sqrt(knorm[reps] + 1e-6)
+    assert norm_rel_err(Kzx_s.cpu().numpy(), ref) < TOL
