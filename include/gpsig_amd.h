@@ -125,8 +125,9 @@ int gpsig_sig_diag(const float *X, int n, int l, int d, int num_levels, int orde
  *   into a DIAG call); gscale (L+1) = dLoss/dscale.  Any of grs1/grs2/gscale may be NULL.
  *   state: NULL, or the buffer a gpsig_sig_gram_state call with the same inputs filled (RECT/UPPER).
  *   Workspace: gpsig_sig_vjp_workspace_bytes(n1, l1, n2, l2, d, num_levels, difference): the feature
- *   records, and for sequences longer than one lane group covers (column blocks) the per-row carries of
- *   one launch chunk.  Any length; d <= 16.
+ *   records, for sequences longer than one lane group covers (column blocks) the per-row carries of
+ *   one launch chunk, and the partial sums of gscale (reduced into gscale after the launch, on the
+ *   same stream).  Any length; d <= 16.
  */
 size_t gpsig_sig_vjp_workspace_bytes(int n1, int l1, int n2, int l2, int d, int num_levels, int difference);
 int gpsig_sig_gram_vjp(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int num_levels,
@@ -201,10 +202,11 @@ int gpsig_pde_diag(const float *X, int n, int l, int d, int dyadic, int solver, 
  * _KdiagGrad; covariance_op/_untrunc_cov_grad.py:25-77): KK = K (.) flip(K_rev) with K_rev solved on the
  * time-reversed paths by the first-order scheme, contracted with the increments.  pair_mode DIAG
  * (gout (n1,), dLoss/dk(x_a, x_a); the reference's factor 2 for the symmetric pair) or RECT (gout
- * (n1, n2); gX and gY).  Accumulates (+=) gX (n1, l1, d), gY (n2, l2, d).  Workspace: the fp64
- * K_rev cells of each evaluated pair (the (I+1) x (J+1) grid, or for J <= 256 the solver's
- * wavefront order, about (I + J/W) J doubles; I = 2^dyadic (l1-1), J = 2^dyadic (l2-1)),
- * gpsig_pde_vjp_workspace_bytes(pairs, l1, l2, dyadic). */
+ * (n1, n2); gX and gY).  Accumulates (+=) gX (n1, l1, d), gY (n2, l2, d).  No grid is stored: K_rev
+ * is re-solved on the mirrored wavefront and meets the forward sweep lane by lane; the workspace holds
+ * the forward sweep's fronts (fp32, every few coarse steps, about (1 + REP/W) I J / H floats per pair;
+ * I = 2^dyadic (l1-1), J = 2^dyadic (l2-1)), gpsig_pde_vjp_workspace_bytes(pairs, l1, l2, dyadic), which
+ * returns 0 where the kernel does not apply (J > 1024 or dyadic > 3: GPSIG_EUNSUPPORTED). */
 size_t gpsig_pde_vjp_workspace_bytes(int npairs, int l1, int l2, int dyadic);
 
 int gpsig_pde_vjp(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int dyadic, int solver,
