@@ -14,6 +14,10 @@
 //     (RBF: k (x - z) for z, k (z - x) for x; linear: x, z) the point gradients: the sequence's are
 //     added per time step (time-major, coalesced across lanes), the tensor's accumulate in registers
 //     and are reduced over the wave at the end.
+// A workgroup is NW waves = NW tensors on the same 64 sequences: the per-step sequence gradients of
+// the NW tensors are summed through LDS and added with one atomic per (time, channel, sequence).  One
+// atomic per tensor before: T * N * L * d * M of them (1.3e9 at T = 512, N = 1024, L = 100, d = 5,
+// M = 5), which at the chip's ~1.3 TB/s of atomic adds was most of the VJP's time.
 // Cells use one exp per component and time step (both sweeps evaluate the same instructions, so the
 // inversion only carries the fp32 rounding of the forward sums).
 #pragma once
@@ -33,35 +37,80 @@ struct TvsBwdArgs {
 // Level I only (levels are independent chains; blockIdx.z selects the level, so the per-lane state is
 // O(I * DP) and not O(M^2 * DP)).  LT below is the number of components of this level.
 // DIFF = false (difference=False): the cells are the point values P_k(s) themselves, s = 0..L-1.
-template <int DP, int I, bool INCR, bool RBF, bool DIFF>
-__device__ __forceinline__ void tvs_bwd_level(const TvsBwdArgs &a) {
+// waves (tensors) per workgroup of the VJP
+template <int DP, bool INCR>
+constexpr int tvs_bwd_waves() { return (DP <= 6 && !INCR) ? 8 : 4; }
+// time steps per staged chunk of the sequence records (x, dx, g of the workgroup's 64 sequences)
+#ifndef GPSIG_TVSB_CS
+#define GPSIG_TVSB_CS 8
+#endif
+template <int DP>
+constexpr int tvs_bwd_chunk() { return DP <= 8 ? GPSIG_TVSB_CS : 2; }
+
+template <int DP, int I, int MMAX, bool INCR, bool RBF, bool DIFF>
+__device__ __forceinline__ void tvs_bwd_level(const TvsBwdArgs &a,
+                                              float (&zl_all)[tvs_bwd_waves<DP, INCR>()][MMAX * 2 * DP],
+                                              float (&red)[2][tvs_bwd_waves<DP, INCR>()][DP][64],
+                                              float (&stg)[2][tvs_bwd_chunk<DP>() + 1][2 * DP + 1][64]) {
   constexpr int LT = I;
+  constexpr int NW = tvs_bwd_waves<DP, INCR>();
   constexpr int KB = I * (I - 1) / 2;  // first component of the level
   constexpr float NHL2E = -0.72134752044448170f;  // exp(-d2/2) = exp2(d2 * NHL2E)
   constexpr float L2E = 1.4426950408889634f;
-  const int lane = threadIdx.x;
-  const int tt = blockIdx.y;
+  const int lane = threadIdx.x & 63;
+  const int wave = wave_uniform(threadIdx.x >> 6);
   const int n = a.n, d = a.d, FC = 2 * d + 3, T = a.t, L = a.l;
+  const int tt0 = blockIdx.y * NW + wave;
+  const bool tvalid = tt0 < T;  // wave-uniform; an idle wave still takes part in every barrier
+  const int tt = tvalid ? tt0 : T - 1;
   const int s0 = blockIdx.x * 64 + lane;
   const bool valid = s0 < n;
   const int sq = valid ? s0 : n - 1;
   const int zs = INCR ? 2 * d : d;
-  // the level's components of this tensor (wave-uniform), staged in LDS: broadcast reads instead of
-  // the serialised L2-latency vector loads the compiler emits for uniform global data it cannot prove
+  // the level's components of this wave's tensor, staged in LDS: broadcast reads instead of the
+  // serialised L2-latency vector loads the compiler emits for uniform global data it cannot prove
   // invariant
-  __shared__ float zl[I * 2 * DP];
+  float *zl = zl_all[wave];
   for (int e = lane; e < I * 2 * DP; e += 64) {
     const int c = e / (2 * DP), h = (e / DP) % 2, q = e % DP;
     zl[e] = (q < d && (INCR || h == 0)) ? a.Z[((long long)(KB + c) * T + tt) * zs + h * d + q] : 0.f;
   }
+  // red: per-step sequence gradients of the NW tensors, summed over the workgroup (double buffered:
+  // one barrier per step)
+  int rbuf = 0;
   __syncthreads();
   // component c of the level (global component KB + c)
   auto z0c = [&](int c, int q) -> float { return zl[(c * 2) * DP + q]; };
   auto z1c = [&](int c, int q) -> float { return zl[(c * 2 + 1) * DP + q]; };
-  auto ld = [&](int s, int c) -> float { return a.Ft[((long long)s * FC + c) * n + sq]; };
-  auto ldx = [&](int s, float (&x)[DP]) {
+  // Sequence records staged through LDS: the workgroup's NW waves share the same 64 sequences, so
+  // each (step, channel) row of 64 floats is fetched once per workgroup by one global_load_lds (an
+  // LDS-DMA, no registers), a chunk of CS steps ahead of its use.  stg[buf][step - c0][slot][lane]:
+  // slots 0..DP-1 = x, DP..2DP-1 = dx, 2DP = g (padded channels are zeroed once, never loaded).
+  constexpr int CS = tvs_bwd_chunk<DP>();
+  const int NCH = 2 * d + 1;
+  for (int e = (int)threadIdx.x; e < 2 * (CS + 1) * 2 * DP * 64; e += NW * 64) {
+    const int l = e & 63, r = e >> 6, slot = r % (2 * DP), si = (r / (2 * DP)) % (CS + 1), b = r / (2 * DP * (CS + 1));
+    if (slot % DP >= d) stg[b][si][slot][l] = 0.f;
+  }
+  // stage steps c0 .. c0 + CS (clamped to the sequence) into stg[buf]
+  auto stage = [&](int buf, int c0) {
+    for (int r = wave; r < (CS + 1) * NCH; r += NW) {
+      const int si = r / NCH, ch = r % NCH;
+      int st = c0 + si;
+      st = st < 0 ? 0 : (st < L ? st : L - 1);
+      const int slot = ch < d ? ch : (ch < 2 * d ? DP + ch - d : 2 * DP);
+      const int gch = ch < 2 * d ? ch : 2 * d + 1;
+      __builtin_amdgcn_global_load_lds(a.Ft + ((long long)st * FC + gch) * n + sq,
+                                       (__attribute__((address_space(3))) void *)&stg[buf][si][slot][0], 4, 0, 0);
+    }
+  };
+  auto ldx = [&](const float (*row)[64], float (&x)[DP]) {
 #pragma unroll
-    for (int q = 0; q < DP; ++q) x[q] = q < d ? ld(s, q) : 0.f;
+    for (int q = 0; q < DP; ++q) x[q] = row[q][lane];
+  };
+  auto lddx = [&](const float (*row)[64], float (&dx)[DP]) {
+#pragma unroll
+    for (int q = 0; q < DP; ++q) dx[q] = row[DP + q][lane];
   };
   auto em1 = [&](float v) -> float {
     return __builtin_fabsf(v) < EM1_TAU ? em1_small(v) : __builtin_amdgcn_exp2f(v * L2E) - 1.0f;
@@ -120,7 +169,7 @@ __device__ __forceinline__ void tvs_bwd_level(const TvsBwdArgs &a) {
     }
   };
 
-  const float gI = valid ? a.gout[((long long)I * T + tt) * n + sq] : 0.f;
+  const float gI = (valid && tvalid) ? a.gout[((long long)I * T + tt) * n + sq] : 0.f;
 
   // ---- forward sweep: end state of the running sums A (index k0 + j - 1 for A_j of level i)
   float A[LT], pv0[LT], pv1[LT];
@@ -137,56 +186,64 @@ __device__ __forceinline__ void tvs_bwd_level(const TvsBwdArgs &a) {
       return v;
     }
   };
-  if constexpr (DIFF) {
-    {
-      float x0[DP];
-      ldx(0, x0);
+  const int nfs = DIFF ? L - 1 : L;  // forward steps
+  int buf = 0;
+  stage(0, 0);
+  for (int c0 = 0; c0 < nfs; c0 += CS) {
+    __syncthreads();  // this chunk has landed (vmcnt(0)); the other buffer is free
+    if (c0 + CS < nfs) stage(buf ^ 1, c0 + CS);
+    const int ce = c0 + CS < nfs ? c0 + CS : nfs;
+    if constexpr (DIFF) {
+      if (c0 == 0) {
+        float x0[DP];
+        ldx(stg[buf][0], x0);
 #pragma unroll
-      for (int k = 0; k < LT; ++k) pvals(k, x0, pv0[k], pv1[k]);
-    }
-    for (int s = 0; s < L - 1; ++s) {
-      float x[DP], dx[DP], xn[DP];
-      ldx(s, x);
+        for (int k = 0; k < LT; ++k) pvals(k, x0, pv0[k], pv1[k]);
+      }
+      for (int s = c0; s < ce; ++s) {
+        float x[DP], dx[DP], xn[DP];
+        ldx(stg[buf][s - c0], x);
+        lddx(stg[buf][s - c0], dx);
+        ldx(stg[buf][s - c0 + 1], xn);
+        const float gs = stg[buf][s - c0][2 * DP][lane];
+        float prev = 0.f;
 #pragma unroll
-      for (int q = 0; q < DP; ++q) dx[q] = q < d ? ld(s, d + q) : 0.f;
-      ldx(s + 1, xn);
-      const float gs = ld(s, 2 * d + 1);
-      float prev = 0.f;
+        for (int k = 0; k < I; ++k) {
+          float n0, n1;
+          pvals(k, xn, n0, n1);
+          const float m = cell(k, x, dx, gs, pv0[k], pv1[k], n0, n1);
+          pv0[k] = n0;
+          pv1[k] = n1;
+          if (k == 0) {
+            prev = m;
+          } else {
+            const float as = A[k - 1];
+            A[k - 1] = as + prev;
+            prev = m * as;
+          }
+        }
+      }
+    } else {
+      for (int s = c0; s < ce; ++s) {
+        float x[DP];
+        ldx(stg[buf][s - c0], x);
+        float prev = 0.f;
 #pragma unroll
-      for (int k = 0; k < I; ++k) {
-        float n0, n1;
-        pvals(k, xn, n0, n1);
-        const float m = cell(k, x, dx, gs, pv0[k], pv1[k], n0, n1);
-        pv0[k] = n0;
-        pv1[k] = n1;
-        if (k == 0) {
-          prev = m;
-        } else {
-          const float as = A[k - 1];
-          A[k - 1] = as + prev;
-          prev = m * as;
+        for (int k = 0; k < I; ++k) {
+          float v0, v1;
+          pvals(k, x, v0, v1);
+          const float m = pcell(k, x, v0, v1);
+          if (k == 0) {
+            prev = m;
+          } else {
+            const float as = A[k - 1];
+            A[k - 1] = as + prev;
+            prev = m * as;
+          }
         }
       }
     }
-  } else {
-    for (int s = 0; s < L; ++s) {
-      float x[DP];
-      ldx(s, x);
-      float prev = 0.f;
-#pragma unroll
-      for (int k = 0; k < I; ++k) {
-        float v0, v1;
-        pvals(k, x, v0, v1);
-        const float m = pcell(k, x, v0, v1);
-        if (k == 0) {
-          prev = m;
-        } else {
-          const float as = A[k - 1];
-          A[k - 1] = as + prev;
-          prev = m * as;
-        }
-      }
-    }
+    buf ^= 1;
   }
 
   // ---- reverse sweep
@@ -237,39 +294,47 @@ __device__ __forceinline__ void tvs_bwd_level(const TvsBwdArgs &a) {
         }
       }
     }
-    if (valid) {
 #pragma unroll
-      for (int q = 0; q < DP; ++q) {
-        const float v = RBF ? __builtin_fmaf(-gxs, xp[q], gxa[q]) : gxa[q];
-        if (q < d) unsafeAtomicAdd(a.gXt + ((long long)sp * d + q) * n + s0, v);
-      }
+    for (int q = 0; q < DP; ++q) red[rbuf][wave][q][lane] = RBF ? __builtin_fmaf(-gxs, xp[q], gxa[q]) : gxa[q];
+    // LDS writes done, then the barrier; no vmcnt wait, so the staged chunk's LDS-DMA stays in flight
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    // the workgroup's sum for (point sp, channel q, sequence) from one thread each
+    for (int e = (int)threadIdx.x; e < DP * 64; e += NW * 64) {
+      const int q = e >> 6, l = e & 63, sqn = (int)blockIdx.x * 64 + l;
+      float v = 0.f;
+#pragma unroll
+      for (int w = 0; w < NW; ++w) v += red[rbuf][w][q][l];
+      if (q < d && sqn < n) unsafeAtomicAdd(a.gXt + ((long long)sp * d + q) * n + sqn, v);
     }
+    rbuf ^= 1;
   };
 
-  // row s of the reverse sweep is loaded one step ahead (before the previous step's atomics)
+  // reverse sweep in chunks of CS steps (descending), each staged one chunk ahead: the chunk with top
+  // step hi holds steps hi - CS + 1 .. hi + 1 (x at s + 1 for the difference cells)
   const int stop = DIFF ? L - 2 : L - 1;  // last row of the grid the recursion consumes
-  float xs1[DP], x[DP], dx[DP], gs;  // xs1 = x at s + 1
-  ldx(L - 1, xs1);
-  ldx(stop, x);
-#pragma unroll
-  for (int q = 0; q < DP; ++q) dx[q] = q < d ? ld(stop, d + q) : 0.f;
-  gs = ld(stop, 2 * d + 1);
-  for (int s = stop; s >= 0; --s) {
-    float xn[DP], dxn[DP], gsn = 0.f;  // row s - 1
-    const int sn = s > 0 ? s - 1 : 0;
-    ldx(sn, xn);
-#pragma unroll
-    for (int q = 0; q < DP; ++q) dxn[q] = q < d ? ld(sn, d + q) : 0.f;
-    gsn = ld(sn, 2 * d + 1);
-    float c0[LT], c1[LT], Ph[LT];
+  float xs1[DP];  // x at s + 1
+  __syncthreads();  // every wave is done with the forward sweep's buffers
+  stage(buf, stop - CS + 1);
+  for (int hi = stop; hi >= 0; hi -= CS) {
+    __syncthreads();  // this chunk has landed; the other buffer is free
+    const int c0 = hi - CS + 1;
+    if (hi - CS >= 0) stage(buf ^ 1, c0 - CS);
+    const int lo = c0 > 0 ? c0 : 0;
+    if (hi == stop) ldx(stg[buf][stop + 1 - c0], xs1);
+    for (int s = hi; s >= lo; --s) {
+    float x[DP], dx[DP];
+    ldx(stg[buf][s - c0], x);
+    lddx(stg[buf][s - c0], dx);
+    const float gs = stg[buf][s - c0][2 * DP][lane];
+    float c0v[LT], c1v[LT], Ph[LT];
     {
       constexpr int i = I, k0 = 0;
       float m[I], Av[I];
 #pragma unroll
       for (int st = 0; st < i; ++st) {
         const int k = k0 + st;
-        pvals(k, x, c0[k], c1[k]);
-        m[st] = DIFF ? cell(k, x, dx, gs, c0[k], c1[k], pv0[k], pv1[k]) : pcell(k, x, c0[k], c1[k]);
+        pvals(k, x, c0v[k], c1v[k]);
+        m[st] = DIFF ? cell(k, x, dx, gs, c0v[k], c1v[k], pv0[k], pv1[k]) : pcell(k, x, c0v[k], c1v[k]);
       }
       // A_j(s) = A_j(s+1) - M_{c_j}(s) A_{j-1}(s), ascending j (A_0 = 1)
       Av[0] = 1.0f;
@@ -297,19 +362,16 @@ __device__ __forceinline__ void tvs_bwd_level(const TvsBwdArgs &a) {
     if constexpr (DIFF)
       emit(s + 1, Ph, pv0, pv1, xs1);
     else
-      emit(s, Ph, c0, c1, x);
+      emit(s, Ph, c0v, c1v, x);
 #pragma unroll
     for (int k = 0; k < LT; ++k) {
-      pv0[k] = c0[k];
-      pv1[k] = c1[k];
+      pv0[k] = c0v[k];
+      pv1[k] = c1v[k];
     }
 #pragma unroll
-    for (int q = 0; q < DP; ++q) {
-      xs1[q] = x[q];
-      x[q] = xn[q];
-      dx[q] = dxn[q];
+    for (int q = 0; q < DP; ++q) xs1[q] = x[q];
     }
-    gs = gsn;
+    buf ^= 1;
   }
   if constexpr (DIFF) {
     float Ph[LT];
@@ -331,7 +393,7 @@ __device__ __forceinline__ void tvs_bwd_level(const TvsBwdArgs &a) {
     r[2 * DP] = S0[k];
     r[2 * DP + 1] = S1[k];
     group_incl_scan_n<64, 2 * DP + 2>(r);
-    if (lane == 63) {
+    if (lane == 63 && tvalid) {
       float *gz = a.gZ + ((long long)(KB + k) * T + tt) * zs;
       for (int q = 0; q < d; ++q) {
         if constexpr (RBF) {
@@ -349,16 +411,21 @@ __device__ __forceinline__ void tvs_bwd_level(const TvsBwdArgs &a) {
 }
 
 template <int DP, int M, bool INCR, bool RBF, bool DIFF>
-__global__ __launch_bounds__(64) void tvs_bwd_kernel(TvsBwdArgs a) {
+__global__ __launch_bounds__((64 * tvs_bwd_waves<DP, INCR>())) void tvs_bwd_kernel(TvsBwdArgs a) {
+  // one LDS allocation for every level's body (declared per level, they would all be allocated)
+  constexpr int NW = tvs_bwd_waves<DP, INCR>();
+  __shared__ float zl_all[NW][M * 2 * DP];
+  __shared__ float red[2][NW][DP][64];
+  __shared__ float stg[2][tvs_bwd_chunk<DP>() + 1][2 * DP + 1][64];
   switch (blockIdx.z) {
-    case 0: tvs_bwd_level<DP, 1, INCR, RBF, DIFF>(a); break;
-    case 1: if constexpr (M >= 2) tvs_bwd_level<DP, 2, INCR, RBF, DIFF>(a); break;
-    case 2: if constexpr (M >= 3) tvs_bwd_level<DP, 3, INCR, RBF, DIFF>(a); break;
-    case 3: if constexpr (M >= 4) tvs_bwd_level<DP, 4, INCR, RBF, DIFF>(a); break;
-    case 4: if constexpr (M >= 5) tvs_bwd_level<DP, 5, INCR, RBF, DIFF>(a); break;
-    case 5: if constexpr (M >= 6) tvs_bwd_level<DP, 6, INCR, RBF, DIFF>(a); break;
-    case 6: if constexpr (M >= 7) tvs_bwd_level<DP, 7, INCR, RBF, DIFF>(a); break;
-    case 7: if constexpr (M >= 8) tvs_bwd_level<DP, 8, INCR, RBF, DIFF>(a); break;
+    case 0: tvs_bwd_level<DP, 1, M, INCR, RBF, DIFF>(a, zl_all, red, stg); break;
+    case 1: if constexpr (M >= 2) tvs_bwd_level<DP, 2, M, INCR, RBF, DIFF>(a, zl_all, red, stg); break;
+    case 2: if constexpr (M >= 3) tvs_bwd_level<DP, 3, M, INCR, RBF, DIFF>(a, zl_all, red, stg); break;
+    case 3: if constexpr (M >= 4) tvs_bwd_level<DP, 4, M, INCR, RBF, DIFF>(a, zl_all, red, stg); break;
+    case 4: if constexpr (M >= 5) tvs_bwd_level<DP, 5, M, INCR, RBF, DIFF>(a, zl_all, red, stg); break;
+    case 5: if constexpr (M >= 6) tvs_bwd_level<DP, 6, M, INCR, RBF, DIFF>(a, zl_all, red, stg); break;
+    case 6: if constexpr (M >= 7) tvs_bwd_level<DP, 7, M, INCR, RBF, DIFF>(a, zl_all, red, stg); break;
+    case 7: if constexpr (M >= 8) tvs_bwd_level<DP, 8, M, INCR, RBF, DIFF>(a, zl_all, red, stg); break;
     default: break;
   }
 }

@@ -9,15 +9,17 @@ namespace gpsig {
 
 template <int DP, int M, bool INCR>
 static int launch_tvs_bwd(const TvsBwdArgs &a, bool rbf, bool diff, hipStream_t s) {
-  const dim3 grid((unsigned)((a.n + 63) / 64), (unsigned)a.t, (unsigned)M);
+  constexpr int NW = tvs_bwd_waves<DP, INCR>();
+  const dim3 grid((unsigned)((a.n + 63) / 64), (unsigned)((a.t + NW - 1) / NW), (unsigned)M);
+  const dim3 block(64 * NW);
   if (rbf && diff)
-    hipLaunchKernelGGL((tvs_bwd_kernel<DP, M, INCR, true, true>), grid, dim3(64), 0, s, a);
+    hipLaunchKernelGGL((tvs_bwd_kernel<DP, M, INCR, true, true>), grid, block, 0, s, a);
   else if (diff)
-    hipLaunchKernelGGL((tvs_bwd_kernel<DP, M, INCR, false, true>), grid, dim3(64), 0, s, a);
+    hipLaunchKernelGGL((tvs_bwd_kernel<DP, M, INCR, false, true>), grid, block, 0, s, a);
   else if (rbf)
-    hipLaunchKernelGGL((tvs_bwd_kernel<DP, M, INCR, true, false>), grid, dim3(64), 0, s, a);
+    hipLaunchKernelGGL((tvs_bwd_kernel<DP, M, INCR, true, false>), grid, block, 0, s, a);
   else
-    hipLaunchKernelGGL((tvs_bwd_kernel<DP, M, INCR, false, false>), grid, dim3(64), 0, s, a);
+    hipLaunchKernelGGL((tvs_bwd_kernel<DP, M, INCR, false, false>), grid, block, 0, s, a);
   return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
 }
 
