@@ -180,8 +180,15 @@ class TensVsSeq(torch.autograd.Function):
     def forward(ctx, Zs, Xs, cfg):
         ctx.cfg = cfg
         ctx.save_for_backward(Zs, Xs)
-        return ops.tens_vs_seq(Zs.detach(), Xs.detach(), cfg["num_levels"], cfg["order"], cfg["base"],
-                               cfg["difference"], cfg["increments"])
+        ctx.state = None
+        args = (Zs.detach(), Xs.detach(), cfg["num_levels"], cfg["order"], cfg["base"], cfg["difference"],
+                cfg["increments"])
+        numel = ops.tens_state_numel(Zs.shape[1], Xs.shape[0], cfg["num_levels"])
+        if any(ctx.needs_input_grad[:2]) and cfg["order"] == 1 and cfg["difference"] and numel * 4 <= GRAM_STATE_BYTES:
+            # the training step keeps the forward's end state: the VJP skips its forward sweep
+            out, ctx.state = ops.tens_vs_seq(*args, state=torch.empty(numel, dtype=torch.float32, device=Xs.device))
+            return out
+        return ops.tens_vs_seq(*args)
 
     @staticmethod
     def backward(ctx, gout):
@@ -189,7 +196,8 @@ class TensVsSeq(torch.autograd.Function):
         _check_bwd(cfg, gram=True)
         Zs, Xs = ctx.saved_tensors
         gZ, gX = ops.tens_vs_seq_vjp(Zs.detach(), Xs.detach(), cfg["num_levels"], gout, cfg["base"],
-                                     cfg["increments"], difference=cfg["difference"])
+                                     cfg["increments"], difference=cfg["difference"], state=ctx.state)
+        ctx.state = None
         return (gZ.to(Zs.dtype) if ctx.needs_input_grad[0] else None,
                 gX.to(Xs.dtype) if ctx.needs_input_grad[1] else None, None)
 

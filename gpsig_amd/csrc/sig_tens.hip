@@ -531,7 +531,7 @@ static int dpad4(int d) { return d <= 4 ? 4 : d <= 8 ? 8 : d <= 16 ? 16 : d <= 3
 
 namespace gpsig {
 int tvs_pk_launch(const float *Z, int lt, int t, int increments, int d, const float *Ft, int n, int l, int M,
-                  float *out, float *Zp, bool rbf, hipStream_t s);
+                  float *out, float *Zp, bool rbf, float *state, hipStream_t s);
 size_t tvs_pk_zp_bytes(int lt, int t, int d);
 }  // namespace gpsig
 
@@ -571,7 +571,7 @@ extern "C" int gpsig_tens_vs_seq(const float *Z, int lt, int t, int increments, 
     // packed fast paths: RBF (exp-free recurrences) and linear
     float *Zp = reinterpret_cast<float *>(static_cast<char *>(workspace) + tvs_ft_bytes(n, l, d));
     const int rc = tvs_pk_launch(Z, lt, t, increments, d, Ft, n, l, num_levels, out, Zp,
-                                 base_kind == GPSIG_BASE_RBF, s);
+                                 base_kind == GPSIG_BASE_RBF, nullptr, s);
     if (rc != -1) return rc;
   }
   TvsArgs a{Z, Ft, lt, t, n, l, d, num_levels, order, increments, difference, base_kind == GPSIG_BASE_RBF, out};
@@ -584,6 +584,28 @@ extern "C" int gpsig_tens_vs_seq(const float *Z, int lt, int t, int increments, 
     default: hipLaunchKernelGGL(tvs_kernel<32>, grid, dim3(64), lds, s, a); break;
   }
   return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
+}
+
+// As gpsig_tens_vs_seq (order 1, difference 1, RBF or linear, d <= 8, num_levels <= 6: the packed fast
+// paths) and also writes the VJP's saved state: state (T, n, LT) = each component's end-of-sweep running
+// sum.  GPSIG_EUNSUPPORTED (nothing launched) outside the fast paths.
+extern "C" int gpsig_tens_vs_seq_state(const float *Z, int lt, int t, int increments, int d, const float *X, int n,
+                                       int l, int num_levels, int base_kind, float *out, float *state, void *workspace,
+                                       size_t workspace_bytes, gpsig_stream_t stream) {
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (!Z || !X || !out || !state || lt <= 0 || t <= 0 || n <= 0 || d <= 0 || num_levels < 1 || l < 2)
+    return GPSIG_EINVAL;
+  if (lt != num_levels * (num_levels + 1) / 2) return GPSIG_EINVAL;
+  if (base_kind != GPSIG_BASE_RBF && base_kind != GPSIG_BASE_LINEAR) return GPSIG_EUNSUPPORTED;
+  if (num_levels > 6 || d > 8 || t > 65535) return GPSIG_EUNSUPPORTED;
+  if (!workspace || workspace_bytes < gpsig_tens_workspace_bytes(n, l, d, lt, t)) return GPSIG_EWORKSPACE;
+  float *Ft = static_cast<float *>(workspace);
+  const long long tot = (long long)n * l;
+  hipLaunchKernelGGL(tvs_features_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, X, n, l, d, Ft);
+  float *Zp = reinterpret_cast<float *>(static_cast<char *>(workspace) + tvs_ft_bytes(n, l, d));
+  const int rc = tvs_pk_launch(Z, lt, t, increments, d, Ft, n, l, num_levels, out, Zp, base_kind == GPSIG_BASE_RBF,
+                               state, s);
+  return rc == -1 ? GPSIG_EUNSUPPORTED : rc;
 }
 
 extern "C" int gpsig_tens_gram(const float *Z, int lt, int t, int increments, int d, int num_levels, int base_kind,

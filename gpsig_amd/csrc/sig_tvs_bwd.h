@@ -32,6 +32,8 @@ struct TvsBwdArgs {
   const float *gout;  // (M+1, T, n) dLoss/dK_m (raw levels)
   float *gZ;          // like Z, accumulated
   float *gXt;         // (l, d, n) time-major, accumulated
+  const float *state; // optional (T, n, LT) end-of-sweep running sums of the forward (gpsig_tens_vs_seq_state):
+                      // the forward sweep is skipped
 };
 
 // Level I only (levels are independent chains; blockIdx.z selects the level, so the per-lane state is
@@ -186,9 +188,16 @@ __device__ __forceinline__ void tvs_bwd_level(const TvsBwdArgs &a,
       return v;
     }
   };
-  const int nfs = DIFF ? L - 1 : L;  // forward steps
+  const int nfs = a.state ? 0 : (DIFF ? L - 1 : L);  // forward steps (none from the saved state)
   int buf = 0;
-  stage(0, 0);
+  if (a.state) {
+    // the forward launch's end state: A_j(L-1) of this level's stages (global components KB + j - 1)
+    const float *st = a.state + ((long long)tt * n + sq) * (MMAX * (MMAX + 1) / 2) + KB;
+#pragma unroll
+    for (int k = 0; k + 1 < LT; ++k) A[k] = st[k];
+  } else {
+    stage(0, 0);
+  }
   for (int c0 = 0; c0 < nfs; c0 += CS) {
     __syncthreads();  // this chunk has landed (vmcnt(0)); the other buffer is free
     if (c0 + CS < nfs) stage(buf ^ 1, c0 + CS);
@@ -320,7 +329,16 @@ __device__ __forceinline__ void tvs_bwd_level(const TvsBwdArgs &a,
     const int c0 = hi - CS + 1;
     if (hi - CS >= 0) stage(buf ^ 1, c0 - CS);
     const int lo = c0 > 0 ? c0 : 0;
-    if (hi == stop) ldx(stg[buf][stop + 1 - c0], xs1);
+    if (hi == stop) {
+      ldx(stg[buf][stop + 1 - c0], xs1);
+      if constexpr (DIFF) {
+        // point values at the last point (left there by the forward sweep, evaluated here from the state)
+        if (a.state) {
+#pragma unroll
+          for (int k = 0; k < LT; ++k) pvals(k, xs1, pv0[k], pv1[k]);
+        }
+      }
+    }
     for (int s = hi; s >= lo; --s) {
     float x[DP], dx[DP];
     ldx(stg[buf][s - c0], x);

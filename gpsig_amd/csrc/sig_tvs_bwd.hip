@@ -32,13 +32,14 @@ extern "C" size_t gpsig_tens_vjp_workspace_bytes(int n, int l, int d) {
 
 extern "C" int gpsig_tens_vs_seq_vjp(const float *Z, int lt, int t, int increments, int d, const float *X, int n,
                                      int l, int num_levels, int base_kind, int difference, const float *gout,
-                                     float *gZ, float *gX,
+                                     float *gZ, float *gX, const float *state,
                                      void *workspace, size_t workspace_bytes, gpsig_stream_t stream) {
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (!Z || !X || !gout || !gZ || !gX || lt <= 0 || t <= 0 || n <= 0 || d <= 0 || l < (difference ? 2 : 1) ||
       num_levels < 1)
     return GPSIG_EINVAL;
   if (lt != num_levels * (num_levels + 1) / 2) return GPSIG_EINVAL;
+  if (state && !difference) return GPSIG_EINVAL;  // the saved state comes from the difference fast paths
   if (base_kind != GPSIG_BASE_RBF && base_kind != GPSIG_BASE_LINEAR) return GPSIG_EUNSUPPORTED;
   const int DP = tvs_bwd_pad(d);
   if (DP == 0 || num_levels > 8 || t > 65535) return GPSIG_EUNSUPPORTED;
@@ -48,7 +49,7 @@ extern "C" int gpsig_tens_vs_seq_vjp(const float *Z, int lt, int t, int incremen
   int rc = tvs_features_launch(X, n, l, d, Ft, s);
   if (rc) return rc;
   if (hipMemsetAsync(gXt, 0, (size_t)n * l * d * sizeof(float), s) != hipSuccess) return GPSIG_ELAUNCH;
-  TvsBwdArgs a{Z, Ft, t, n, l, d, gout, gZ, gXt};
+  TvsBwdArgs a{Z, Ft, t, n, l, d, gout, gZ, gXt, state};
   const bool rbf = base_kind == GPSIG_BASE_RBF;
   switch (DP * 2 + (increments ? 1 : 0)) {
     case 4: rc = tvs_bwd_launch_dp<2, false>(a, num_levels, rbf, difference != 0, s); break;

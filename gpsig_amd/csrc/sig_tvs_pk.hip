@@ -22,6 +22,8 @@ struct TvsPkArgs {
   const float *Ft;  // time-major features Ft[(s * FC + c) * n + seq], FC = 2d + 3 (sig_tens.hip)
   int t, n, l, d;
   float *out;       // (M+1, T, n)
+  float *state;     // optional (T, n, LT): end-of-sweep running sums of every component (the VJP's
+                    // saved state, gpsig_tens_vs_seq_state)
 };
 
 template <int DP, bool INCR>
@@ -227,6 +229,16 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(INCR ? GPSIG
       for (int i = 1; i <= M; ++i) a.out[((long long)i * a.t + tt) * n + sq] = K[i][h];
     }
   }
+  if (a.state) {  // the end-of-sweep running sums: the VJP starts at its reverse sweep
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int sq = h ? s1 : s0;
+      if (sq < n) {
+#pragma unroll
+        for (int k = 0; k < LT; ++k) a.state[((long long)tt * n + sq) * LT + k] = Ss[k][h];
+      }
+    }
+  }
 }
 
 // Linear base kernel (kernels.py:979-986), difference=True: the seed of component k at time cell s is
@@ -288,14 +300,24 @@ __global__ __launch_bounds__(64) void tvs_lin_kernel(TvsPkArgs a) {
       for (int i = 1; i <= M; ++i) a.out[((long long)i * a.t + tt) * n + sq] = K[i][h];
     }
   }
+  if (a.state) {  // the end-of-sweep running sums: the VJP starts at its reverse sweep
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int sq = h ? s1 : s0;
+      if (sq < n) {
+#pragma unroll
+        for (int k = 0; k < LT; ++k) a.state[((long long)tt * n + sq) * LT + k] = Ss[k][h];
+      }
+    }
+  }
 }
 
 template <int DP, int M, bool INCR>
 static int launch_tvs_pk(const float *Z, int lt, int t, int d, const float *Ft, int n, int l, float *out, float *Zp,
-                         bool rbf, hipStream_t s) {
+                         bool rbf, float *state, hipStream_t s) {
   hipLaunchKernelGGL((tvs_prep_kernel<DP, INCR>), dim3((unsigned)((lt * t + 255) / 256)), dim3(256), 0, s, Z, lt, t, d,
                      Zp);
-  TvsPkArgs a{Zp, Ft, t, n, l, d, out};
+  TvsPkArgs a{Zp, Ft, t, n, l, d, out, state};
   if (rbf)
     hipLaunchKernelGGL((tvs_pk_kernel<DP, M, INCR>), dim3((unsigned)((n + 127) / 128), (unsigned)t), dim3(64), 0, s, a);
   else
@@ -305,27 +327,27 @@ static int launch_tvs_pk(const float *Z, int lt, int t, int d, const float *Ft, 
 
 template <int DP, bool INCR>
 static int tvs_pk_m(int M, const float *Z, int lt, int t, int d, const float *Ft, int n, int l, float *out, float *Zp,
-                    bool rbf, hipStream_t s) {
+                    bool rbf, float *state, hipStream_t s) {
   switch (M) {
-    case 1: return launch_tvs_pk<DP, 1, INCR>(Z, lt, t, d, Ft, n, l, out, Zp, rbf, s);
-    case 2: return launch_tvs_pk<DP, 2, INCR>(Z, lt, t, d, Ft, n, l, out, Zp, rbf, s);
-    case 3: return launch_tvs_pk<DP, 3, INCR>(Z, lt, t, d, Ft, n, l, out, Zp, rbf, s);
-    case 4: return launch_tvs_pk<DP, 4, INCR>(Z, lt, t, d, Ft, n, l, out, Zp, rbf, s);
-    case 5: return launch_tvs_pk<DP, 5, INCR>(Z, lt, t, d, Ft, n, l, out, Zp, rbf, s);
-    case 6: return launch_tvs_pk<DP, 6, INCR>(Z, lt, t, d, Ft, n, l, out, Zp, rbf, s);
+    case 1: return launch_tvs_pk<DP, 1, INCR>(Z, lt, t, d, Ft, n, l, out, Zp, rbf, state, s);
+    case 2: return launch_tvs_pk<DP, 2, INCR>(Z, lt, t, d, Ft, n, l, out, Zp, rbf, state, s);
+    case 3: return launch_tvs_pk<DP, 3, INCR>(Z, lt, t, d, Ft, n, l, out, Zp, rbf, state, s);
+    case 4: return launch_tvs_pk<DP, 4, INCR>(Z, lt, t, d, Ft, n, l, out, Zp, rbf, state, s);
+    case 5: return launch_tvs_pk<DP, 5, INCR>(Z, lt, t, d, Ft, n, l, out, Zp, rbf, state, s);
+    case 6: return launch_tvs_pk<DP, 6, INCR>(Z, lt, t, d, Ft, n, l, out, Zp, rbf, state, s);
     default: return -1;
   }
 }
 
 // -1: not covered by the fast path (the caller runs the general kernel)
 int tvs_pk_launch(const float *Z, int lt, int t, int increments, int d, const float *Ft, int n, int l, int M,
-                  float *out, float *Zp, bool rbf, hipStream_t s) {
+                  float *out, float *Zp, bool rbf, float *state, hipStream_t s) {
   if (M > 6 || d > 8 || l < 2) return -1;
   const int DP = d;
 #define GPSIG_TVS(dp)                                                               \
   case dp:                                                                          \
-    return increments ? tvs_pk_m<dp, true>(M, Z, lt, t, d, Ft, n, l, out, Zp, rbf, s)    \
-                      : tvs_pk_m<dp, false>(M, Z, lt, t, d, Ft, n, l, out, Zp, rbf, s);
+    return increments ? tvs_pk_m<dp, true>(M, Z, lt, t, d, Ft, n, l, out, Zp, rbf, state, s)    \
+                      : tvs_pk_m<dp, false>(M, Z, lt, t, d, Ft, n, l, out, Zp, rbf, state, s);
   switch (DP) {
     GPSIG_TVS(1) GPSIG_TVS(2) GPSIG_TVS(3) GPSIG_TVS(4) GPSIG_TVS(5) GPSIG_TVS(6) GPSIG_TVS(7) GPSIG_TVS(8)
     default: return -1;

@@ -367,8 +367,10 @@ def sym_assemble(src: torch.Tensor, row_off: torch.Tensor, level_stride: int, n:
 
 # ----------------------------------------------------------------------------- inducing tensors
 def tens_vs_seq(Z: torch.Tensor, X: torch.Tensor, num_levels: int, order: int = 1, base="rbf",
-                difference: bool = True, increments: bool = False) -> torch.Tensor:
-    """<z_t, S(x_n)> per level: Z (LT,T,D) or (LT,T,2,D) with increments, X (N,L,D) -> (M+1, T, N)."""
+                difference: bool = True, increments: bool = False, state: torch.Tensor | None = None):
+    """<z_t, S(x_n)> per level: Z (LT,T,D) or (LT,T,2,D) with increments, X (N,L,D) -> (M+1, T, N).
+    state: a float32 buffer of tens_state_numel(...) elements -> also the VJP's saved state
+    (gpsig_tens_vs_seq_state); returns (out, state) then, state None where the fast paths do not apply."""
     _require_cuda(Z, X)
     lib = L.load()
     Z, X = _f32(Z), _f32(X)
@@ -380,6 +382,18 @@ def tens_vs_seq(Z: torch.Tensor, X: torch.Tensor, num_levels: int, order: int = 
         raise ValueError(f"Z must have num_levels*(num_levels+1)/2 = {num_levels * (num_levels + 1) // 2} components")
     out = torch.empty((num_levels + 1, t, n), dtype=torch.float32, device=X.device)
     ws = workspace(X.device, lib.gpsig_tens_workspace_bytes(n, l, d, lt, t))
+    if state is not None:
+        if state.dtype != torch.float32 or not state.is_contiguous() or state.numel() < t * n * lt:
+            raise ValueError("state must be a contiguous float32 buffer of tens_state_numel() elements")
+        rc = L.GPSIG_EUNSUPPORTED
+        if order == 1 and difference:
+            rc = lib.gpsig_tens_vs_seq_state(Z.data_ptr(), lt, t, int(increments), d, X.data_ptr(), n, l, num_levels,
+                                             base_kind(base), out.data_ptr(), state.data_ptr(), ws.data_ptr(),
+                                             ws.numel(), _stream(X.device))
+        if rc != L.GPSIG_EUNSUPPORTED:
+            L.check(rc, "gpsig_tens_vs_seq_state")
+            return out, state
+        return tens_vs_seq(Z, X, num_levels, order, base, difference, increments), None
     rc = lib.gpsig_tens_vs_seq(Z.data_ptr(), lt, t, int(increments), d, X.data_ptr(), n, l, num_levels, order,
                                base_kind(base), int(difference), out.data_ptr(), ws.data_ptr(), ws.numel(),
                                _stream(X.device))
@@ -387,9 +401,14 @@ def tens_vs_seq(Z: torch.Tensor, X: torch.Tensor, num_levels: int, order: int = 
     return out
 
 
+def tens_state_numel(t: int, n: int, num_levels: int) -> int:
+    """Floats of the tens_vs_seq VJP's saved state: (T, N, LT)."""
+    return t * n * (num_levels * (num_levels + 1) // 2)
+
+
 def tens_vs_seq_vjp(Z: torch.Tensor, X: torch.Tensor, num_levels: int, gout: torch.Tensor, base="rbf",
                     increments: bool = False, gZ: torch.Tensor | None = None, gX: torch.Tensor | None = None,
-                    difference: bool = True):
+                    difference: bool = True, state: torch.Tensor | None = None):
     """dLoss/dZ, dLoss/dX of the raw per-level tens_vs_seq output (order 1, difference True or False) given
     gout (num_levels+1, T, N); accumulated into float32 buffers (see gpsig_tens_vs_seq_vjp)."""
     _require_cuda(Z, X, gout)
@@ -409,7 +428,7 @@ def tens_vs_seq_vjp(Z: torch.Tensor, X: torch.Tensor, num_levels: int, gout: tor
     ws = workspace(X.device, lib.gpsig_tens_vjp_workspace_bytes(n, l, d))
     rc = lib.gpsig_tens_vs_seq_vjp(Z.data_ptr(), lt, t, int(increments), d, X.data_ptr(), n, l, num_levels,
                                    base_kind(base), int(bool(difference)), gout.data_ptr(), gZ.data_ptr(),
-                                   gX.data_ptr(), ws.data_ptr(),
+                                   gX.data_ptr(), _ptr(state), ws.data_ptr(),
                                    ws.numel(), _stream(X.device))
     L.check(rc, "gpsig_tens_vs_seq_vjp")
     return gZ, gX

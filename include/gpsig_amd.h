@@ -167,15 +167,26 @@ int gpsig_tens_gram(const float *Z, int lt, int t, int increments, int d, int nu
 int gpsig_tens_gram_vjp(const float *Z, int lt, int t, int increments, int d, int num_levels, int base_kind,
                         const float *gout, float *gZ, gpsig_stream_t stream);
 
+/* gpsig_tens_vs_seq for a training step: the same output (order 1, difference 1, RBF or linear, d <= 8,
+ * num_levels <= 6 -- the packed fast paths; GPSIG_EUNSUPPORTED otherwise, nothing launched) plus the
+ * VJP's saved state: state (T, n, LT) = every component's end-of-sweep running sum (the TF graph's
+ * saved intermediates for autodiff of _K_tens_vs_seq, kernels.py:314-341).  Workspace as
+ * gpsig_tens_vs_seq. */
+int gpsig_tens_vs_seq_state(const float *Z, int lt, int t, int increments, int d, const float *X, int n, int l,
+                            int num_levels, int base_kind, float *out, float *state, void *workspace,
+                            size_t workspace_bytes, gpsig_stream_t stream);
+
 /* Gradient of gpsig_tens_vs_seq (order 1, difference 1 or 0, RBF or linear, num_levels <= 8, d <= 16):
  * the reference differentiates _K_tens_vs_seq (kernels.py:314-341 + signature_algs.py:101-127) by TF
  * autodiff.  gout (num_levels+1, T, n) = dLoss/d(raw per-level output); accumulates (+=) gZ (same
- * layout as Z) and gX (n, l, d).  Workspace: gpsig_tens_vjp_workspace_bytes(n, l, d). */
+ * layout as Z) and gX (n, l, d).  state: NULL, or the buffer a gpsig_tens_vs_seq_state call on the same
+ * inputs filled (difference 1): the VJP then skips its forward sweep.  Workspace:
+ * gpsig_tens_vjp_workspace_bytes(n, l, d). */
 size_t gpsig_tens_vjp_workspace_bytes(int n, int l, int d);
 
 int gpsig_tens_vs_seq_vjp(const float *Z, int lt, int t, int increments, int d, const float *X, int n, int l,
                           int num_levels, int base_kind, int difference, const float *gout, float *gZ, float *gX,
-                          void *workspace, size_t workspace_bytes, gpsig_stream_t stream);
+                          const float *state, void *workspace, size_t workspace_bytes, gpsig_stream_t stream);
 
 size_t gpsig_rescaled_workspace_bytes(int n, int num_levels);
 

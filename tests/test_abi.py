@@ -75,8 +75,10 @@ def test_vjp_and_feature_entry_points_validate_arguments():
     assert lib.gpsig_sig_state_bytes(4, 6, 10, 5, L.PAIRS_RECT) == 4 * 6 * (4 * 9 + 5) * 4
     assert lib.gpsig_sig_state_bytes(6, 6, 10, 5, L.PAIRS_UPPER) == 21 * (4 * 9 + 5) * 4
     assert lib.gpsig_sig_state_bytes(6, 6, 10, 5, L.PAIRS_DIAG) == 0
-    assert lib.gpsig_tens_vs_seq_vjp(None, 6, 2, 0, 3, None, 4, 10, 3, 0, 1, None, None, None, None, 0,
+    assert lib.gpsig_tens_vs_seq_vjp(None, 6, 2, 0, 3, None, 4, 10, 3, 0, 1, None, None, None, None, None, 0,
                                      None) == L.GPSIG_EINVAL
+    assert lib.gpsig_tens_vs_seq_state(None, 6, 2, 0, 3, None, 4, 10, 3, 0, None, None, None, 0,
+                                       None) == L.GPSIG_EINVAL
     assert lib.gpsig_tens_gram_vjp(None, 6, 2, 0, 3, 3, 0, None, None, None) == L.GPSIG_EINVAL
     assert lib.gpsig_pde_vjp(None, 4, 10, None, 4, 10, 3, 0, 1, 0, 0, 4, None, None, None, None, 0,
                              None) == L.GPSIG_EINVAL

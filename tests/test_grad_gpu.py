@@ -352,3 +352,27 @@ def test_K_tens_n_seq_covs_gradient():
     assert norm_rel_err(Zt.grad.cpu().numpy(), Zr.grad.numpy()) < GTOL
     assert norm_rel_err(Xt.grad.reshape(X.shape).cpu().numpy(), Xr.grad.numpy()) < GTOL
     assert norm_rel_err(k.variances.grad.cpu().numpy(), vr.grad.numpy()) < GTOL
+
+
+@pytest.mark.parametrize("base", ["rbf", "linear"])
+@pytest.mark.parametrize("increments", [False, True])
+def test_tens_vs_seq_saved_state_vjp_equals_recompute(base, increments):
+    """The Kuf VJP from the forward launch's saved end state (gpsig_tens_vs_seq_state) equals the VJP
+    that recomputes its forward sweep (the forward's exp-free recurrences vs the VJP's exact cells: fp32
+    rounding only); the state path's output equals the plain launch bit for bit."""
+    from gpsig_amd import ops
+    T, N, L, D, M = 33, 130, 60, 5, 5
+    LT = M * (M + 1) // 2
+    rng = np.random.default_rng(40)
+    Z = torch.tensor(0.5 * rng.standard_normal((LT, T, 2, D) if increments else (LT, T, D)), device=DEV,
+                     dtype=torch.float32)
+    X = torch.tensor(walks(N, L, D, 41), device=DEV, dtype=torch.float32)
+    G = torch.randn(M + 1, T, N, device=DEV)
+    st = torch.empty(ops.tens_state_numel(T, N, M), device=DEV)
+    out, st2 = ops.tens_vs_seq(Z, X, M, 1, base, True, increments, state=st)
+    assert st2 is st
+    torch.testing.assert_close(out, ops.tens_vs_seq(Z, X, M, 1, base, True, increments), rtol=0, atol=0)
+    gz0, gx0 = ops.tens_vs_seq_vjp(Z, X, M, G, base, increments)
+    gz1, gx1 = ops.tens_vs_seq_vjp(Z, X, M, G, base, increments, state=st)
+    assert norm_rel_err(gz1.cpu().numpy(), gz0.cpu().numpy()) < 1e-5
+    assert norm_rel_err(gx1.cpu().numpy(), gx0.cpu().numpy()) < 1e-5
