@@ -22,6 +22,15 @@ struct SigFeatArgs {
   int total;       // sum_{m=1}^{depth} d^m
 };
 
+// Digits of a multi-index in base d (indices < 2^32 / d; tensors here are < 2^14 entries): quotient by a multiply-high with
+// ceil(2^32 / d) instead of an integer division (a runtime division is a ~20-instruction sequence, and
+// the digit loops run per tensor entry, per increment).
+struct DivD {
+  unsigned m, d;
+  __device__ explicit DivD(int dd) : m(0xFFFFFFFFu / (unsigned)dd + 1u), d((unsigned)dd) {}
+  __device__ int div(int v) const { return d == 1 ? v : (int)__umulhi((unsigned)v, m); }
+};
+
 __global__ __launch_bounds__(256) void sig_features_kernel(SigFeatArgs a) {
   extern __shared__ __attribute__((aligned(16))) float S[];  // [h (d) | level 1 | level 2 | ...]
   const int path = blockIdx.x, tid = threadIdx.x, nth = blockDim.x;
@@ -37,6 +46,7 @@ __global__ __launch_bounds__(256) void sig_features_kernel(SigFeatArgs a) {
     if (m < M) off[m + 1] = off[m] + sz[m];
   }
   const float *x = a.X + (long long)path * a.l * d;
+  const DivD dv(d);
   for (int s = 0; s + 1 < a.l; ++s) {
     __syncthreads();
     if (tid < d) h[tid] = x[(s + 1) * d + tid] - x[s * d + tid];
@@ -47,8 +57,8 @@ __global__ __launch_bounds__(256) void sig_features_kernel(SigFeatArgs a) {
         float acc = 0.0f, P = 1.0f, fact = 1.0f;
         int pre = e;
         for (int j = m - 1; j >= 0; --j) {
-          const int digit = pre % d;
-          pre /= d;
+          const int q = dv.div(pre), digit = pre - q * d;
+          pre = q;
           P *= h[digit];
           fact *= (float)(m - j);
           const float Sj = (j == 0) ? 1.0f : lev[off[j] + pre];
@@ -71,8 +81,20 @@ __global__ __launch_bounds__(256) void sig_features_kernel(SigFeatArgs a) {
 //   dE_r[v]  = sum_{m>=r} sum_u dT_m[u v] S_{m-r}[u]
 //   dS_j[u]  = sum_{m>=j} sum_v dT_m[u v] E_{m-j}[v]          (in place, ascending j)
 //   dh[q]    = sum_r sum_v dE_r[v] dE_r[v]/dh[q],  E_r[v] = h[v_1] ... h[v_r] / r!
-// and dx_{k+1} += dh, dx_k -= dh.  LDS: h, dh, S, dS, dE.
+// and dx_{k+1} += dh, dx_k -= dh.  LDS: h, dh, S, dS, dE, E.
 constexpr int GH_REG = 8;  // channels whose increment gradient is accumulated in registers
+
+// lanes per output when `outputs` sums share a wave: the largest power of two G <= 64 / outputs
+__device__ inline int group_lanes(int outputs) {
+  int G = 1;
+  while (G < 64 && 2 * G * outputs <= 64) G *= 2;
+  return G;
+}
+// sum over aligned groups of G lanes (every lane of the wave takes part)
+__device__ inline float group_reduce(float v, int G) {
+  for (int o = G / 2; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
 
 __global__ __launch_bounds__(256) void sig_features_bwd_kernel(SigFeatArgs a, const float *__restrict__ gout,
                                                                float *__restrict__ gX) {
@@ -89,6 +111,7 @@ __global__ __launch_bounds__(256) void sig_features_bwd_kernel(SigFeatArgs a, co
     if (m < M) off[m + 1] = off[m] + sz[m];
   }
   const float *x = a.X + (long long)path * a.l * d;
+  const DivD dv(d);
   float *gx = gX + (long long)path * a.l * d;
   const float *g = gout + (long long)path * tot;
   for (int e = tid; e < tot; e += nth) {
@@ -103,8 +126,8 @@ __global__ __launch_bounds__(256) void sig_features_bwd_kernel(SigFeatArgs a, co
         float acc = 0.0f, P = 1.0f, fact = 1.0f;
         int pre = e;
         for (int j = m - 1; j >= 0; --j) {
-          const int digit = pre % d;
-          pre /= d;
+          const int q = dv.div(pre), digit = pre - q * d;
+          pre = q;
           P *= h[digit];
           fact *= (float)(m - j);
           const float Sj = (j == 0) ? 1.0f : lev[off[j] + pre];
@@ -115,15 +138,21 @@ __global__ __launch_bounds__(256) void sig_features_bwd_kernel(SigFeatArgs a, co
       __syncthreads();
     }
   };
-  // E_r[v] = prod h[v_p] / r!
-  auto Ev = [&](int r, int v) -> float {
-    float P = 1.0f, fact = 1.0f;
-    for (int p = 0; p < r; ++p) {
-      P *= h[v % d];
-      v /= d;
-      fact *= (float)(p + 1);
-    }
-    return P / fact;
+  // E_r[v] = prod h[v_p] / r!, tabulated per increment in LDS (Et, same layout as the levels)
+  float *Et = gE + tot;
+  auto fill_E = [&]() {
+    for (int r = 1; r <= M; ++r)
+      for (int v = tid; v < sz[r]; v += nth) {
+        float P = 1.0f, fact = 1.0f;
+        int w = v;
+        for (int p = 0; p < r; ++p) {
+          const int q = dv.div(w);
+          P *= h[w - q * d];
+          w = q;
+          fact *= (float)(p + 1);
+        }
+        Et[off[r] + v] = P / fact;
+      }
   };
   for (int s = 0; s + 1 < a.l; ++s) {
     __syncthreads();
@@ -140,20 +169,28 @@ __global__ __launch_bounds__(256) void sig_features_bwd_kernel(SigFeatArgs a, co
     chen();  // lev = S before increment s
     if (tid < d) h[tid] = -h[tid];
     __syncthreads();
-    // dE_r[v] for r = 1..M
-    for (int r = 1; r <= M; ++r)
-      for (int v = tid; v < sz[r]; v += nth) {
+    fill_E();
+    // dE_r[v] for r = 1..M.  The low levels have few outputs with long sums: each output gets a group of
+    // G lanes (G = the largest power of two with G * outputs <= the wave) that split its terms and
+    // reduce them by xor-shuffles, so the wave stays busy.
+    for (int r = 1; r <= M; ++r) {
+      const int G = group_lanes(sz[r]), g = tid & (G - 1);
+      for (int ob = 0; ob < sz[r]; ob += nth / G) {
+        const int v = ob + tid / G;
         float acc = 0.0f;
-        for (int m = r; m <= M; ++m) {
-          const int nu = sz[m - r];
-          const float *Tm = adj + off[m];
-          for (int u = 0; u < nu; ++u) {
-            const float Su = (m == r) ? 1.0f : lev[off[m - r] + u];
-            acc = __builtin_fmaf(Tm[u * sz[r] + v], Su, acc);
+        if (v < sz[r])
+          for (int m = r; m <= M; ++m) {
+            const int nu = sz[m - r];
+            const float *Tm = adj + off[m];
+            for (int u = g; u < nu; u += G) {
+              const float Su = (m == r) ? 1.0f : lev[off[m - r] + u];
+              acc = __builtin_fmaf(Tm[u * sz[r] + v], Su, acc);
+            }
           }
-        }
-        gE[off[r] + v] = acc;
+        acc = group_reduce(acc, G);
+        if (v < sz[r] && g == 0) gE[off[r] + v] = acc;
       }
+    }
     __syncthreads();
     // dh from dE: per-thread partials in registers (d <= GH_REG), reduced over the wave and added
     // to the d LDS slots by one lane per wave; wider paths take LDS atomics
@@ -168,13 +205,14 @@ __global__ __launch_bounds__(256) void sig_features_bwd_kernel(SigFeatArgs a, co
         // digits of v (most significant first is irrelevant: the product is symmetric)
         int vv = v;
         for (int p = 0; p < r; ++p) {
-          const int q = vv % d;
-          vv /= d;
+          const int vq = dv.div(vv), q = vv - vq * d;
+          vv = vq;
           float P = 1.0f;
           int w = v;
           for (int p2 = 0; p2 < r; ++p2) {
-            if (p2 != p) P *= h[w % d];
-            w /= d;
+            const int wq = dv.div(w);
+            if (p2 != p) P *= h[w - wq * d];
+            w = wq;
           }
           const float val = ge * P / fact;
           if (d <= GH_REG) {
@@ -192,16 +230,23 @@ __global__ __launch_bounds__(256) void sig_features_bwd_kernel(SigFeatArgs a, co
         for (int q = 0; q < GH_REG; ++q)
           if (q < d) atomicAdd(gh + q, ghr[q]);
     }
-    // dS_j[u] = sum_{m>=j} sum_v dT_m[u v] E_{m-j}[v], ascending j in place
+    // dS_j[u] = sum_{m>=j} sum_v dT_m[u v] E_{m-j}[v], ascending j in place (grouped as dE)
     for (int j = 1; j <= M; ++j) {
-      for (int u = tid; u < sz[j]; u += nth) {
-        float acc = adj[off[j] + u];
-        for (int m = j + 1; m <= M; ++m) {
-          const int nv = sz[m - j];
-          const float *Tm = adj + off[m];
-          for (int v = 0; v < nv; ++v) acc = __builtin_fmaf(Tm[u * nv + v], Ev(m - j, v), acc);
+      const int G = group_lanes(sz[j]), g = tid & (G - 1);
+      for (int ob = 0; ob < sz[j]; ob += nth / G) {
+        const int u = ob + tid / G;
+        float acc = 0.0f;
+        if (u < sz[j]) {
+          if (g == 0) acc = adj[off[j] + u];
+          for (int m = j + 1; m <= M; ++m) {
+            const int nv = sz[m - j];
+            const float *Tm = adj + off[m];
+            const float *E = Et + off[m - j];
+            for (int v = g; v < nv; v += G) acc = __builtin_fmaf(Tm[u * nv + v], E[v], acc);
+          }
         }
-        adj[off[j] + u] = acc;
+        acc = group_reduce(acc, G);
+        if (u < sz[j] && g == 0) adj[off[j] + u] = acc;
       }
       __syncthreads();
     }
@@ -226,7 +271,7 @@ extern "C" int gpsig_signature_vjp(const float *X, int n, int l, int d, int dept
     p *= d;
     total += p;
   }
-  const size_t lds = (size_t)(3 * total + 2 * d) * sizeof(float);
+  const size_t lds = (size_t)(4 * total + 2 * d) * sizeof(float);
   if (lds > 64 * 1024) return GPSIG_EUNSUPPORTED;
   SigFeatArgs a{X, n, l, d, depth, nullptr, (int)total};
   // one wave per path while the top level fits a few entries per lane (barriers stay wave-local)
