@@ -213,9 +213,9 @@ def main():
     avg_launch_s = kern_ms / 1e3 / max(launches, 1)
     achieved = entries_per_launch * b_entry / avg_launch_s / 1e9
     traffic, prof = None, {}
-    # the committed profile is of the default workload and seed engine; other runs report traffic null
+    # the committed profile is of the default single-GPU launch; other runs report traffic null
     if (args.traffic_json and os.path.exists(args.traffic_json) and args.workload == "H" and not args.n
-            and args.seed_engine == "valu"):
+            and args.seed_engine == "valu" and world == 1):
         with open(args.traffic_json) as f:
             prof = json.load(f)
         traffic = prof.get("hbm_bytes_per_launch")
