@@ -128,6 +128,9 @@ def main():
     ap.add_argument("--no-probe", action="store_true", help="skip the HBM copy-bandwidth probe")
     ap.add_argument("--seed-engine", default="valu", choices=["valu", "mfma"],
                     help="RBF seed dots on packed VALU FMAs (default) or on the matrix cores (A/B arm)")
+    ap.add_argument("--gram-path", default="fused", choices=["fused", "split"],
+                    help="fused Gram kernel (default) or the split diagnostic of SURVEY.md 8d: a producer "
+                         "launch writes the cells dM to HBM, a consumer streams them through the recursion")
     ap.add_argument("--backend", default="nccl",
                     help="process-group backend (nccl = RCCL; gloo only to rehearse N>1 ranks on one GPU)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r2_gram_counters.json"),
@@ -176,7 +179,8 @@ def main():
         rows_done[0] += (a1 - a0) * n - (a1 * (a1 - 1) - a0 * (a0 - 1)) // 2
         return r
 
-    gram_base = L.BASE_RBF | (L.BASE_SEED_MFMA if args.seed_engine == "mfma" else 0)
+    gram_base = (L.BASE_RBF | (L.BASE_SEED_MFMA if args.seed_engine == "mfma" else 0)
+                 | (L.GRAM_SPLIT if args.gram_path == "split" else 0))
 
     def step():
         Xs = kern._prep(X)
@@ -215,7 +219,7 @@ def main():
     traffic, prof = None, {}
     # the committed profile is of the default single-GPU launch; other runs report traffic null
     if (args.traffic_json and os.path.exists(args.traffic_json) and args.workload == "H" and not args.n
-            and args.seed_engine == "valu" and world == 1):
+            and args.seed_engine == "valu" and args.gram_path == "fused" and world == 1):
         with open(args.traffic_json) as f:
             prof = json.load(f)
         traffic = prof.get("hbm_bytes_per_launch")
@@ -239,7 +243,8 @@ def main():
                    "global_batch": n, "seq_len": l, "parallelism": f"row-shard{world}" if world > 1 else "single"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "sig_fo_kernel", "seed_engine": args.seed_engine, "launch_ms": avg_launch_s * 1e3, "bytes_per_entry": b_entry,
+                     "kernel": "sig_fo_kernel", "seed_engine": args.seed_engine, "gram_path": args.gram_path,
+                     "launch_ms": avg_launch_s * 1e3, "bytes_per_entry": b_entry,
                      "entries_per_launch": entries_per_launch,
                      # the fused kernel never materialises the tile: physically it is VALU-issue bound
                      "physical_bound": "valu", "valu_busy": prof.get("valu_busy"),

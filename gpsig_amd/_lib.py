@@ -34,6 +34,7 @@ _ERRORS = {
 BASE_RBF = 0
 BASE_LINEAR = 1
 BASE_SEED_MFMA = 0x100  # flag: RBF seed dots on the matrix cores (A/B arm, include/gpsig_amd.h)
+GRAM_SPLIT = 0x200  # flag: split producer/consumer diagnostic of the first-order Gram (include/gpsig_amd.h)
 PAIRS_RECT, PAIRS_UPPER, PAIRS_DIAG = 0, 1, 2
 OUT_LEVELS, OUT_NORM_LEVELS, OUT_NORM_SUM, OUT_RSQRT = 0, 1, 2, 3
 
@@ -44,6 +45,7 @@ _SZ = ctypes.c_size_t
 
 SIGNATURES = {
     "gpsig_sig_workspace_bytes": (_SZ, [_I, _I, _I, _I, _I]),
+    "gpsig_sig_split_bytes": (_SZ, [_I, _I, _I, _I]),
     "gpsig_sig_vjp_workspace_bytes": (_SZ, [_I, _I, _I, _I, _I, _I, _I]),
     "gpsig_sig_gram": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I,
                             _P, _P, _P, _F, _I, _P, _I, _I, _P, _SZ, _P]),

@@ -6,6 +6,7 @@ namespace gpsig {
 int features(const float *X, int n, int l, int d, int DP, float *F, hipStream_t s);
 int sig_fo_launch(const SigArgs &a, int DP, int seed, long long nblocks, hipStream_t s);
 int fo_lanes_per_pair(int l2, int DP, int M, bool mf);
+size_t fo_split_bytes(int l1, int l2, int DP, int M);
 int sig_ho_launch(const SigArgs &a, int DP, int seed, long long nblocks, hipStream_t s);
 int ho_lanes_per_pair(int l2, int order, int M);
 int pde_launch(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int dyadic, int solver,
@@ -46,6 +47,12 @@ extern "C" size_t gpsig_sig_workspace_bytes(int n1, int l1, int n2, int l2, int 
   return feat_bytes(n1, l1, d) + feat_bytes(n2, l2, d);
 }
 
+extern "C" size_t gpsig_sig_split_bytes(int l1, int l2, int d, int num_levels) {
+  const int DP = pad_channels(d, 1);
+  if (DP == 0 || l1 < 2 || l2 < 2 || num_levels < 1 || num_levels > 8) return 0;
+  return fo_split_bytes(l1, l2, DP, num_levels);
+}
+
 static inline long long upper_prefix(long long r, long long ntb, long long k) { return r * ntb - k * r * (r - 1) / 2; }
 
 static int sig_gram_impl(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int num_levels,
@@ -64,9 +71,12 @@ static int sig_gram_impl(const float *X, int n1, int l1, const float *Y, int n2,
   if ((rs1 == nullptr) != (rs2 == nullptr)) return GPSIG_EINVAL;
   if (order < 1) return GPSIG_EINVAL;
   const bool mfma = (base_kind & GPSIG_BASE_SEED_MFMA) != 0;
-  base_kind &= ~GPSIG_BASE_SEED_MFMA;
+  const bool split = (base_kind & GPSIG_GRAM_SPLIT) != 0;
+  base_kind &= ~(GPSIG_BASE_SEED_MFMA | GPSIG_GRAM_SPLIT);
   const int seed = seed_of(base_kind, difference);
   if (mfma && (seed != SEED_RBF_DIFF || order != 1 || state)) return GPSIG_EUNSUPPORTED;
+  if (split && (mfma || seed != SEED_RBF_DIFF || order != 1 || state || pair_mode == GPSIG_PAIRS_DIAG))
+    return GPSIG_EUNSUPPORTED;
   const int DP = pad_channels(d, order);
   if (seed < 0 || DP == 0) return GPSIG_EUNSUPPORTED;
   if (row_end == row_begin) return GPSIG_OK;
@@ -74,7 +84,9 @@ static int sig_gram_impl(const float *X, int n1, int l1, const float *Y, int n2,
   const bool same = (X == Y && n1 == n2 && l1 == l2);
   const size_t fx_b = align256((size_t)n1 * l1 * feat_stride(DP) * sizeof(float));
   const size_t fy_b = same ? 0 : align256((size_t)n2 * l2 * feat_stride(DP) * sizeof(float));
-  if (!workspace || workspace_bytes < fx_b + fy_b) return GPSIG_EWORKSPACE;
+  const size_t dm_b = split ? gpsig_sig_split_bytes(l1, l2, d, num_levels) : 0;
+  if (split && dm_b == 0) return GPSIG_EUNSUPPORTED;
+  if (!workspace || workspace_bytes < fx_b + fy_b + dm_b) return GPSIG_EWORKSPACE;
   float *FX = static_cast<float *>(workspace);
   float *FY = same ? FX : reinterpret_cast<float *>(static_cast<char *>(workspace) + fx_b);
   int rc = features(X, n1, l1, d, DP, FX, s);
@@ -101,6 +113,7 @@ static int sig_gram_impl(const float *X, int n1, int l1, const float *Y, int n2,
   a.out_lvl = (long long)out_rows * n2;
   a.state = state;
   a.mfma = mfma ? 1 : 0;
+  a.dmbuf = split ? reinterpret_cast<float *>(static_cast<char *>(workspace) + fx_b + fy_b) : nullptr;
 
   const int LP = (order == 1) ? fo_lanes_per_pair(l2, DP, num_levels, mfma) : ho_lanes_per_pair(l2, order, num_levels);
   if (LP == 0) return GPSIG_EUNSUPPORTED;

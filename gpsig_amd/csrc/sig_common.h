@@ -37,6 +37,11 @@ struct SigArgs {
   float *state;               // optional saved forward state for the VJP (gpsig_sig_gram_state)
   int mfma;                   // RBF difference seed: increment dots on the matrix cores (GPSIG_BASE_SEED_MFMA)
   int nblk;                   // column blocks per pair (first order, LP = 64; 1 = unblocked)
+  // split diagnostic (GPSIG_GRAM_SPLIT): a producer launch writes each pair's cells dM to
+  // dmbuf, a consumer launch streams them through the recursion; blk0 = first logical workgroup of a
+  // chunked launch, dmbuf slot of a pair = its workgroup-local index
+  float *dmbuf;
+  long long blk0;
 };
 
 // Saved forward state of a first-order pair (gpsig_sig_gram_state): column sums of levels 1..M-1

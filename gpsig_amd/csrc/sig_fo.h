@@ -23,7 +23,9 @@ namespace gpsig {
 // (gpsig_sig_gram_state) -- a separate instantiation, so the plain Gram keeps its register budget.
 // MF: the increment inner products of the RBF seed on the matrix cores (RbfSeedPk::mfma_pc), 4 rows
 // per batch, instead of packed VALU dots.
-template <int DP, int W, int LP, int M, int SEED, bool DIAGK, bool SAVE = false, bool MF = false>
+// SPLIT (diagnostic, SURVEY.md 8d "split design"): 1 = producer (cells dM of every row to p.dmbuf, no
+// recursion, no output), 2 = consumer (cells streamed from p.dmbuf through the recursion and epilogue).
+template <int DP, int W, int LP, int M, int SEED, bool DIAGK, bool SAVE = false, bool MF = false, int SPLIT = 0>
 #ifdef GPSIG_FO_LB
 #define GPSIG_FO_BOUNDS __launch_bounds__(256, GPSIG_FO_LB)
 #else
@@ -47,18 +49,24 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
     if (a >= p.row_end) return;
   } else {
     int ta, tb;
+    const long long lblk = p.blk0 + (long long)blockIdx.x;
     if (p.pair_mode == GPSIG_PAIRS_UPPER) {
-      const Tile t = upper_tile(p.tile_base + (long long)blockIdx.x, p.ntb, 4 / G);
+      const Tile t = upper_tile(p.tile_base + lblk, p.ntb, 4 / G);
       ta = t.ta;
       tb = t.tb;
     } else {
-      ta = p.tiles_a0 + (int)blockIdx.x / p.ntb;
-      tb = (int)blockIdx.x % p.ntb;
+      ta = p.tiles_a0 + (int)(lblk / p.ntb);
+      tb = (int)(lblk % p.ntb);
     }
     a = ta * 4 + wave;
     b = tb * G + g;
     if (a < p.row_begin || a >= p.row_end) return;  // wave-uniform
   }
+  static_assert(SPLIT == 0 || (!DIAGK && !SAVE && !MF && SEED == SEED_RBF_DIFF), "split: RBF Gram pairs only");
+  // split: this pair's cell slab, [row][lane of the group][W] (each lane's W cells contiguous)
+  float *__restrict__ dms = nullptr;
+  if constexpr (SPLIT != 0)
+    dms = p.dmbuf + (((long long)blockIdx.x * 4 + wave) * G + g) * (long long)(p.l1 - 1) * (LP * W) + (long long)gl * W;
   bool pair_ok = b < p.n2;
   if (p.pair_mode == GPSIG_PAIRS_UPPER) pair_ok = pair_ok && b >= a;
   if (DIAGK) pair_ok = (g == 0);
@@ -106,7 +114,15 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
     using Rec = std::conditional_t<PK, typename RbfSeedPk<DP, W>::Row, RowData<DP>>;
     auto do_row = [&](int i, const Rec &rd, bool anch, const f2 *pc = nullptr) {
       f2 dM[W2];
-      if constexpr (PK) {
+      if constexpr (SPLIT == 2) {
+        const f4 *src = reinterpret_cast<const f4 *>(dms + (long long)i * (LP * W));
+#pragma unroll
+        for (int w4 = 0; w4 < W / 4; ++w4) {
+          const f4 v = __builtin_nontemporal_load(src + w4);
+          dM[2 * w4] = (f2){v[0], v[1]};
+          dM[2 * w4 + 1] = (f2){v[2], v[3]};
+        }
+      } else if constexpr (PK) {
         if (MF && pc) {
           f2 pp[W2], cc[W2];
 #pragma unroll
@@ -123,6 +139,13 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
         seed.template row<true>(rd, d1);
 #pragma unroll
         for (int w2 = 0; w2 < W2; ++w2) dM[w2] = (f2){d1[w2], d1[w2 + W2]};
+      }
+      if constexpr (SPLIT == 1) {
+        f4 *dst = reinterpret_cast<f4 *>(dms + (long long)i * (LP * W));
+#pragma unroll
+        for (int w4 = 0; w4 < W / 4; ++w4)
+          __builtin_nontemporal_store((f4){dM[2 * w4][0], dM[2 * w4][1], dM[2 * w4 + 1][0], dM[2 * w4 + 1][1]}, dst + w4);
+        return;
       }
       // Column pair k of a lane holds columns (k, k + W/2), so the in-lane exclusive prefix runs on both
       // halves at once: E_k = P_0 + ... + P_{k-1} (packed), E_{W/2} = (H_lo, H_hi) the half totals, and
@@ -242,6 +265,7 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
     }
   }
 
+  if constexpr (SPLIT == 1) return;  // the producer stores no output
   // ---- epilogue
   float K[M + 1];
   K[0] = 1.0f;
@@ -317,6 +341,27 @@ int launch_fo(const SigArgs &a, long long nblocks, hipStream_t s) {
   return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
 }
 
+// Workgroups per launch chunk of the split diagnostic: dmbuf holds FO_SPLIT_BLOCKS * 4 * G pairs'
+// cells, (l1 - 1) x LP * W floats each.
+constexpr long long FO_SPLIT_BLOCKS = 4096;
+
+template <int DP, int W, int LP, int M, int SEED>
+int launch_fo_split(const SigArgs &a0, long long nblocks, hipStream_t s) {
+  if constexpr (SEED != SEED_RBF_DIFF || W % 4 != 0) {
+    return GPSIG_EUNSUPPORTED;
+  } else {
+    if (a0.nblk != 1 || a0.pair_mode == GPSIG_PAIRS_DIAG || a0.state || !a0.dmbuf) return GPSIG_EUNSUPPORTED;
+    SigArgs a = a0;
+    for (long long c = 0; c < nblocks; c += FO_SPLIT_BLOCKS) {
+      a.blk0 = c;
+      const long long nb = nblocks - c < FO_SPLIT_BLOCKS ? nblocks - c : FO_SPLIT_BLOCKS;
+      hipLaunchKernelGGL((sig_fo_kernel<DP, W, LP, M, SEED, false, false, false, 1>), dim3((unsigned)nb), dim3(256), 0, s, a);
+      hipLaunchKernelGGL((sig_fo_kernel<DP, W, LP, M, SEED, false, false, false, 2>), dim3((unsigned)nb), dim3(256), 0, s, a);
+    }
+    return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
+  }
+}
+
 template <int DP, int M, int SEED>
 int fo_geo(const SigArgs &a, long long nblocks, hipStream_t s) {
   const Geo geo = fo_geometry(a.l2, DP, M, a.mfma != 0);
@@ -331,6 +376,16 @@ int fo_geo(const SigArgs &a, long long nblocks, hipStream_t s) {
   }
   if (a.mfma) return GPSIG_EUNSUPPORTED;
   constexpr int WM = fo_wmax(DP, M);
+  if (a.dmbuf) {  // split diagnostic
+    if constexpr (SEED == SEED_RBF_DIFF && WM >= 4) {
+#define GPSIG_GEO(w, lp) \
+  if (geo.W == w && geo.LP == lp) return launch_fo_split<DP, w, lp, M, SEED>(a, nblocks, s);
+      GPSIG_GEO(4, 16) GPSIG_GEO(4, 32) GPSIG_GEO(4, 64)
+      if constexpr (WM >= 8) { GPSIG_GEO(8, 16) GPSIG_GEO(8, 32) GPSIG_GEO(8, 64) }
+#undef GPSIG_GEO
+    }
+    return GPSIG_EUNSUPPORTED;
+  }
 #define GPSIG_GEO(w, lp) \
   if (geo.W == w && geo.LP == lp) return launch_fo<DP, w, lp, M, SEED>(a, nblocks, s);
   GPSIG_GEO(2, 16) GPSIG_GEO(2, 32) GPSIG_GEO(2, 64)

@@ -94,4 +94,12 @@ int sig_fo_launch(const SigArgs &a0, int DP, int seed, long long nblocks, hipStr
 
 int fo_lanes_per_pair(int l2, int DP, int M, bool mf) { return fo_geometry(l2, DP, M, mf).LP; }
 
+// one chunk of the split diagnostic: FO_SPLIT_BLOCKS workgroups x 4 waves x G pairs, (l1 - 1) rows of
+// LP * W cells each (0: the geometry has column blocks or W < 4, where the split does not apply)
+size_t fo_split_bytes(int l1, int l2, int DP, int M) {
+  const Geo g = fo_geometry(l2, DP, M, false);
+  if (g.W < 4 || fo_blocks(l2, true, g) != 1) return 0;
+  return (size_t)FO_SPLIT_BLOCKS * 4 * (64 / g.LP) * (size_t)(l1 - 1) * g.LP * g.W * sizeof(float);
+}
+
 }  // namespace gpsig

@@ -115,6 +115,8 @@ def sig_gram(X: torch.Tensor, Y: torch.Tensor | None, num_levels: int, order: in
     if scale is not None:
         scale = _f32(scale)
     nb = lib.gpsig_sig_workspace_bytes(n1, l1, n2, l2, d)
+    if base_kind(base) & L.GRAM_SPLIT:  # split diagnostic: one chunk of pairs' cells in the workspace
+        nb += lib.gpsig_sig_split_bytes(l1, l2, d, num_levels)
     ws = workspace(X.device, nb)
     pm = L.PAIRS_UPPER if sym else L.PAIRS_RECT
     if state is not None:

@@ -45,7 +45,14 @@ enum gpsig_base_kind {
    * state): evaluate the seed's increment inner products <y_j, dx_i>, <dy_j, dx_i> (the reference's
    * seed GEMM, kernels.py:946-957 + 1042-1044) on the matrix cores (v_mfma_f32_4x4x1_16b_f32) instead of
    * packed VALU FMAs.  Bitwise the same results; slower on MI355X, kept as the A/B arm. */
-  GPSIG_BASE_SEED_MFMA = 0x100
+  GPSIG_BASE_SEED_MFMA = 0x100,
+  /* Flag OR-ed into base_kind of gpsig_sig_gram (RBF, order 1, difference 1, Gram pairs, no saved state,
+   * sequences within one lane group): the split design of SURVEY.md 8d as a diagnostic -- a producer
+   * launch writes every pair's cells dM (fp32) to the workspace, a consumer launch streams them from HBM
+   * through the recursion, in chunks of pairs.  Same results as the fused kernel; the consumer's HBM
+   * traffic is the recursion's algorithmic bytes.  Workspace: gpsig_sig_workspace_bytes(...) +
+   * gpsig_sig_split_bytes(...). */
+  GPSIG_GRAM_SPLIT = 0x200
 };
 
 /* Which (a, b) sequence pairs a Gram call evaluates. */
@@ -81,6 +88,8 @@ enum gpsig_out_mode {
  *     entry (b, a) is also stored when b lies in that row window.
  */
 size_t gpsig_sig_workspace_bytes(int n1, int l1, int n2, int l2, int d);
+/* Extra workspace of a GPSIG_GRAM_SPLIT call (one chunk of pairs' cells); 0 where the split does not apply. */
+size_t gpsig_sig_split_bytes(int l1, int l2, int d, int num_levels);
 
 int gpsig_sig_gram(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int num_levels,
                    int order, int base_kind, int difference, int pair_mode, int row_begin, int row_end,

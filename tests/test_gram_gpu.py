@@ -205,3 +205,22 @@ def test_mfma_seed_arm_matches_valu_arm(L, D, M):
     dm = ops.sig_diag(t(X), M, base=mf).cpu().numpy()
     dv = ops.sig_diag(t(X), M).cpu().numpy()
     assert (norm_rel_err(dm[1:], dv[1:], axis_levels=True) < 5e-6).all()
+
+
+@pytest.mark.parametrize("N,L,D,M", [(70, 50, 3, 4), (40, 128, 5, 5), (36, 100, 8, 6)])
+def test_split_diagnostic_matches_fused(N, L, D, M):
+    """The split design of SURVEY.md 8d (GPSIG_GRAM_SPLIT: producer writes the cells dM to HBM, consumer
+    streams them through the recursion) gives the fused kernel's Gram: same cell instructions, same
+    recursion; K(X) (upper pairs, mirror) and K(X, X2), raw levels and the fused normalised sum."""
+    from gpsig_amd import _lib as Lb
+    from gpsig_amd import ops
+
+    def walks(n, seed):
+        rng = np.random.default_rng(seed)
+        return np.cumsum(rng.standard_normal((n, L, D)), axis=1) / np.sqrt(L * D)
+    X = torch.as_tensor(walks(N, 7), device=DEV, dtype=torch.float32)
+    Y = torch.as_tensor(walks(N // 2 + 3, 8), device=DEV, dtype=torch.float32)
+    for Yt in (None, Y):
+        ref = ops.sig_gram(X, Yt, M, base=Lb.BASE_RBF)
+        got = ops.sig_gram(X, Yt, M, base=Lb.BASE_RBF | Lb.GRAM_SPLIT)
+        torch.testing.assert_close(got, ref, rtol=0, atol=1e-6 * float(ref.abs().max()))
