@@ -81,10 +81,11 @@ def test_pde_cross_vjp_matches_adjoint(n):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("L,n", [(100, 1), (200, 1), (129, 2), (300, 1)])
+@pytest.mark.parametrize("L,n", [(100, 1), (200, 1), (129, 2), (300, 1), (500, 0), (500, 1)])
 def test_pde_kdiag_vjp_wide_grids(L, n):
-    """Wide grids of the adjoint kernel: 2^n (L-1) = 198 (W = 4, step-ordered K_rev cells), 398 and 512
-    (W = 8) and 598 refined columns (W = 16, row-major K_rev cells with the reversed read)."""
+    """Wide grids of the adjoint kernel: 2^n (L-1) = 198 (W = 4), 398 and 512 (W = 8), 598 refined
+    columns (W = 16), and the reference's VOSF training length (train_gpsig_vosf.py:25,100: max_len 500,
+    UntruncSignatureKernel order 0; order 1 = 998 refined columns)."""
     from gpsig_amd import ops
     rng = np.random.default_rng(L + n)
     X = np.cumsum(rng.standard_normal((3, L, 3)), 1) / np.sqrt(L * 3) * 2
