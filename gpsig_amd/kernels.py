@@ -540,6 +540,17 @@ class SignatureKernel:
     def compute_K_incr_tens_vs_seq(self, Z, X):
         return self.K_tens_vs_seq(_as_tensor(Z), _as_tensor(X), increments=True, return_levels=False).cpu().numpy()
 
+    def compute_base_kern_symm(self, X):
+        """kernels.py:151-158: the base-kernel tensor M[a, b, i, j] = k(x_{a,i}, x_{b,j}) of the scaled
+        sequences, (N, N, L, L) -- the tensor the reference's recursion consumes (here for inspection
+        only: the gfx950 kernels never materialise it)."""
+        Xt = _as_tensor(X)
+        N = Xt.shape[0]
+        Xs = self._apply_scaling_and_lags_to_sequences(Xt.reshape(N, -1, self.num_features)).to(torch.float64)
+        Ln = Xs.shape[1]
+        P = Xs.reshape(N * Ln, -1)
+        return self._base_kern(P).reshape(N, Ln, N, Ln).permute(0, 2, 1, 3).cpu().numpy()
+
 
 def _tensor_inner_product(M, num_levels):
     """signature_algs_vosf.py:51-74."""

@@ -124,6 +124,28 @@ class UntruncSignatureKernel:
         """Reference kernels_pde.py:110-112 returns Kdiag here."""
         return self.Kdiag(_as_tensor(X)).cpu().numpy()
 
+    # autoflow helpers of the VOSF terms (kernels_pde.py:114-133), NumPy out
+    def compute_inner_product_tens_vs_seq(self, Z, X):
+        return self.inner_product_tens_vs_seq(_as_tensor(Z), _as_tensor(X)).cpu().numpy()
+
+    def compute_mahalanobis_terms_approx_posterior(self, Z, X):
+        return self.Mahalanobis_term_approx_posterior(_as_tensor(Z), _as_tensor(X)).cpu().numpy()
+
+    def compute_norms_tens(self, Z):
+        return self.norms_tens(_as_tensor(Z)).cpu().numpy()
+
+    def compute_logs_tens(self, Z):
+        return self.logs_tens(_as_tensor(Z)).cpu().numpy()
+
+    def compute_K_base(self, X):
+        """kernels_pde.py:130-133: the state-space embedding's Gram of each point set of X (B, n, D) ->
+        (B, n, n) (RBF exp(-|x - y|^2 / 2) or linear <x, y>, kernels_pde.py:392-438)."""
+        Xt = _as_tensor(X).to(torch.float64)
+        if self._embedding() == "rbf":
+            sq = (Xt ** 2).sum(-1)
+            return torch.exp(-(sq[..., :, None] + sq[..., None, :] - 2.0 * Xt @ Xt.transpose(-1, -2)) / 2).cpu().numpy()
+        return (Xt @ Xt.transpose(-1, -2)).cpu().numpy()
+
     # ------------------------------------------------------------------ VOSF helpers (kernels_pde.py:191-387)
     def _embedding(self):
         if self.base is None:

@@ -178,3 +178,32 @@ def test_inducing_variables_mirror(increments):
     e = ref.K_seq_n_seq_covs(Zs.reshape(4, -1), X.reshape(N, -1))
     for a, b in zip((Kzz, Kzx, Kxx), e):
         assert norm_rel_err(a.cpu().numpy(), b) < TOL
+
+
+def test_autoflow_helpers():
+    """The reference's autoflow helpers (kernels.py:151-158; kernels_pde.py:114-133) return NumPy equal to
+    the methods they wrap; the base-kernel tensor and the per-set base Gram against NumPy."""
+    import gpsig_amd
+    from gpsig_amd import kernels_pde as kp
+    g = golden("rescaled.npz")
+    X, Z, M = g["X"], g["Z"], int(g["num_levels"])
+    N, L, D = X.shape
+    Zfull = np.concatenate([np.full((1, Z.shape[1], D), 0.7), Z], axis=0)
+    ls = np.linspace(0.8, 1.2, D)
+    k = gpsig_amd.SignatureRBF(L * D, D, M, lengthscales=ls)
+    Mb = k.compute_base_kern_symm(X.reshape(N, -1))
+    P = X / ls
+    sq = ((P[:, None, :, None, :] - P[None, :, None, :, :]) ** 2).sum(-1)
+    np.testing.assert_allclose(Mb, np.exp(-sq / 2), rtol=1e-10, atol=1e-12)
+    for emb_cls in (kp.SignatureRBF, kp.SignatureLinear):
+        kv = emb_cls(L * D, D, order=M, num_levels=M)
+        Xf, Zt = t(X.reshape(N, -1)), t(Zfull)
+        np.testing.assert_allclose(kv.compute_inner_product_tens_vs_seq(Zfull, X.reshape(N, -1)),
+                                   kv.inner_product_tens_vs_seq(Zt, Xf).cpu().numpy())
+        np.testing.assert_allclose(kv.compute_mahalanobis_terms_approx_posterior(Zfull, X.reshape(N, -1)),
+                                   kv.Mahalanobis_term_approx_posterior(Zt, Xf).cpu().numpy())
+        np.testing.assert_allclose(kv.compute_norms_tens(Zfull), kv.norms_tens(Zt).cpu().numpy())
+        np.testing.assert_allclose(kv.compute_logs_tens(np.abs(Zfull) + 0.1), kv.logs_tens(t(np.abs(Zfull) + 0.1)).cpu().numpy())
+        Kb = kv.compute_K_base(X)
+        exp = np.exp(-((X[:, :, None] - X[:, None]) ** 2).sum(-1) / 2) if kv.base == "rbf" else X @ X.transpose(0, 2, 1)
+        np.testing.assert_allclose(Kb, exp, rtol=1e-10, atol=1e-12)
