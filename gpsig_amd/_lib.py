@@ -59,6 +59,8 @@ SIGNATURES = {
     "gpsig_pde_diag": (_I, [_P, _I, _I, _I, _I, _I, _P, _P]),
     "gpsig_pde_vjp_workspace_bytes": (_SZ, [_I, _I, _I, _I]),
     "gpsig_pde_vjp": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _SZ, _P]),
+    "gpsig_pde_fronts": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _SZ, _P]),
+    "gpsig_pde_vjp_fronts": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _SZ, _P]),
     "gpsig_sym_assemble": (_I, [_P, _P, ctypes.c_longlong, _I, _I, _P, _P]),
     "gpsig_tens_vs_seq": (_I, [_P, _I, _I, _I, _I, _P, _I, _I, _I, _I, _I, _I, _P, _P, _SZ, _P]),
     "gpsig_tens_gram": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P]),

@@ -220,6 +220,20 @@ class TensGram(torch.autograd.Function):
         return gZ.to(Zs.dtype), None
 
 
+PDE_FRONTS_BYTES = int(os.environ.get("GPSIG_PDE_FRONTS_BYTES", 16 << 30))
+
+
+def _pde_fronts_buffer(ctx, Xs, npairs, l1, l2, dyadic):
+    """Buffer for the PDE adjoint's forward fronts when a gradient is needed and they fit
+    PDE_FRONTS_BYTES (env GPSIG_PDE_FRONTS_BYTES); None: the backward recomputes them."""
+    if not any(ctx.needs_input_grad[:2]):
+        return None
+    nb = ops.pde_fronts_bytes(npairs, l1, l2, dyadic)
+    if nb == 0 or nb > PDE_FRONTS_BYTES:
+        return None
+    return torch.empty((nb + 3) // 4, dtype=torch.float32, device=Xs.device)
+
+
 class PdeDiag(torch.autograd.Function):
     """k(x_a, x_a) of the Goursat PDE (UntruncSignatureKernel.Kdiag) with the reference's adjoint
     (kernels_pde.py:465-509) as backward (gpsig_pde_vjp, DIAG)."""
@@ -228,12 +242,19 @@ class PdeDiag(torch.autograd.Function):
     def forward(ctx, Xs, dyadic, solver):
         ctx.dyadic, ctx.solver = dyadic, solver
         ctx.save_for_backward(Xs)
+        ctx.fronts = _pde_fronts_buffer(ctx, Xs, Xs.shape[0], Xs.shape[1], Xs.shape[1], dyadic)
+        if ctx.fronts is not None:  # the training step's forward keeps the adjoint's fronts
+            return ops.pde_fronts(Xs.detach(), None, dyadic, solver, ctx.fronts, diag=True)
         return ops.pde_diag(Xs.detach(), dyadic, solver)
 
     @staticmethod
     def backward(ctx, gout):
         (Xs,) = ctx.saved_tensors
-        gX = ops.pde_diag_vjp(Xs.detach(), gout, ctx.dyadic, ctx.solver)
+        if ctx.fronts is not None:
+            gX = ops.pde_vjp_fronts(Xs.detach(), None, gout, ctx.dyadic, ctx.solver, ctx.fronts, diag=True)
+            ctx.fronts = None
+        else:
+            gX = ops.pde_diag_vjp(Xs.detach(), gout, ctx.dyadic, ctx.solver)
         return gX.to(Xs.dtype), None, None
 
 
@@ -244,12 +265,22 @@ class PdeGram(torch.autograd.Function):
     def forward(ctx, Xs, X2s, dyadic, solver):
         ctx.dyadic, ctx.solver = dyadic, solver
         ctx.save_for_backward(Xs, X2s)
-        return ops.pde_gram(Xs.detach(), None if X2s is None else X2s.detach(), dyadic, solver)
+        Y = Xs if X2s is None else X2s
+        ctx.fronts = _pde_fronts_buffer(ctx, Xs, Xs.shape[0] * Y.shape[0], Xs.shape[1], Y.shape[1], dyadic)
+        X2d = None if X2s is None else X2s.detach()
+        if ctx.fronts is not None:  # the training step's forward keeps the adjoint's fronts
+            return ops.pde_fronts(Xs.detach(), X2d, dyadic, solver, ctx.fronts)
+        return ops.pde_gram(Xs.detach(), X2d, dyadic, solver)
 
     @staticmethod
     def backward(ctx, gout):
         Xs, X2s = ctx.saved_tensors
-        gX, gY = ops.pde_gram_vjp(Xs.detach(), None if X2s is None else X2s.detach(), gout, ctx.dyadic, ctx.solver)
+        X2d = None if X2s is None else X2s.detach()
+        if ctx.fronts is not None:
+            gX, gY = ops.pde_vjp_fronts(Xs.detach(), X2d, gout, ctx.dyadic, ctx.solver, ctx.fronts)
+            ctx.fronts = None
+        else:
+            gX, gY = ops.pde_gram_vjp(Xs.detach(), X2d, gout, ctx.dyadic, ctx.solver)
         return (gX.to(Xs.dtype), None if gY is None else gY.to(X2s.dtype), None, None)
 
 

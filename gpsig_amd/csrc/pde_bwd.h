@@ -44,6 +44,8 @@ struct PdeBwdArgs {
   const float *gout;  // DIAG: (n1,); RECT: (n1, n2)
   float *gX, *gY;     // accumulated (n1, l1, d), (n2, l2, d)
   float *fronts;      // workspace: per evaluated pair, nfronts x (W + REP) x 64 floats (pde_front_floats)
+  float *out;         // MODE 1 (forward with fronts): K per pair, DIAG out[a - row_begin], RECT
+                      // out[(a - row_begin) * n2 + b]
 };
 
 GPSIG_DEV double lane_next_d(double v) { return dpp_d<0x130>(v); }
@@ -72,7 +74,10 @@ inline long long pde_front_floats(int l1, int l2, int dyadic) {
   return nfr * (W + rep) * 64;
 }
 
-template <int DP, int W, int REP, bool COLS>
+// MODE 0: both passes (gpsig_pde_vjp); 1: pass A only, plus the kernel value K[I][J] of every pair (the
+// forward of a training step, gpsig_pde_fronts); 2: pass B only, from the fronts a MODE 1 launch left
+// (gpsig_pde_vjp_fronts).
+template <int DP, int W, int REP, bool COLS, int MODE = 0>
 __global__ __launch_bounds__(256) void pde_adj_kernel(PdeBwdArgs p) {
   static_assert(W % REP == 0, "a lane owns whole coarse columns");
   constexpr int WC = W / REP;
@@ -125,6 +130,11 @@ __global__ __launch_bounds__(256) void pde_adj_kernel(PdeBwdArgs p) {
 #pragma unroll
     for (int k = 0; k < DP; ++k) dy[w][k] = k < d ? y[(cj + 1) * d + k] - y[cj * d + k] : 0.0f;
   }
+  double dyd[WC][DP];  // fp64 copies for the contractions (converted once, not per cell)
+#pragma unroll
+  for (int w = 0; w < WC; ++w)
+#pragma unroll
+    for (int k = 0; k < DP; ++k) dyd[w][k] = (double)dy[w][k];
   __syncthreads();
 
   const bool s1 = p.solver == 1;
@@ -199,7 +209,7 @@ __global__ __launch_bounds__(256) void pde_adj_kernel(PdeBwdArgs p) {
   for (int r = 0; r < REP; ++r) last[r] = 1.0;
   corner_prev = 1.0;
   const int nst = ok ? nsteps : 0;  // invalid waves still reach the barrier below
-  for (int s0 = 0; s0 < nst; s0 += H) {
+  for (int s0 = 0; MODE != 2 && s0 < nst; s0 += H) {
     float *f = fr + (long long)(s0 / H) * FW * 64;
 #pragma unroll
     for (int w = 0; w < W; ++w) f[w * 64 + lane] = (float)up[w];
@@ -213,6 +223,19 @@ __global__ __launch_bounds__(256) void pde_adj_kernel(PdeBwdArgs p) {
     }
   }
 
+  if constexpr (MODE == 1) {
+    // K[I][J] = the last row's value in fine column J - 1 (the forward op's value: same cells)
+    const int owner = (J - 1) / W, slot = (J - 1) % W;
+    double res = 0.0;
+#pragma unroll
+    for (int w = 0; w < W; ++w)
+      if (w == slot) res = up[w];
+    if (ok && lane == owner) {
+      if (diag) p.out[a - p.row_begin] = (float)res;
+      else p.out[(long long)(a - p.row_begin) * p.n2 + b] = (float)res;
+    }
+    return;
+  }
   // ---- pass B: chunks backwards; the R sweep runs continuously in its own step order
   double ru[W], rlast[REP], rcorner = 1.0;
   double gcol[WC][DP];
@@ -274,15 +297,18 @@ __global__ __launch_bounds__(256) void pde_adj_kernel(PdeBwdArgs p) {
           }
           rlast[r] = rgt;
         }
-        double grow[DP];
+        double grow[DP], dxd[DP];
 #pragma unroll
-        for (int k = 0; k < DP; ++k) grow[k] = 0.0;
+        for (int k = 0; k < DP; ++k) {
+          grow[k] = 0.0;
+          dxd[k] = (double)dxv[k];
+        }
 #pragma unroll
         for (int w = 0; w < WC; ++w)
 #pragma unroll
           for (int k = 0; k < DP; ++k) {
-            grow[k] = __builtin_fma(S[w], (double)dy[w][k], grow[k]);
-            if constexpr (COLS) gcol[w][k] = __builtin_fma(S[w], (double)dxv[k], gcol[w][k]);
+            grow[k] = __builtin_fma(S[w], dyd[w][k], grow[k]);
+            if constexpr (COLS) gcol[w][k] = __builtin_fma(S[w], dxd[k], gcol[w][k]);
           }
 #pragma unroll
         for (int k = 0; k < DP; ++k)
@@ -322,7 +348,7 @@ __global__ __launch_bounds__(256) void pde_adj_kernel(PdeBwdArgs p) {
   }
 }
 
-template <int DP, int W, int REP>
+template <int DP, int W, int REP, int MODE>
 static int launch_pde_adj(const PdeBwdArgs &a, long long nblocks, hipStream_t s) {
   if constexpr (W < REP || REP * W > 64) {
     return GPSIG_EUNSUPPORTED;
@@ -330,37 +356,47 @@ static int launch_pde_adj(const PdeBwdArgs &a, long long nblocks, hipStream_t s)
     const size_t lds = (size_t)4 * (a.l1 - 1) * DP * 2 * sizeof(double);
     if (lds > 160 * 1024) return GPSIG_EUNSUPPORTED;
     // the column (dK/dy) accumulators only for cross pairs; k(x, x) takes twice the row part
-    if (a.pair_mode == GPSIG_PAIRS_DIAG)
-      hipLaunchKernelGGL((pde_adj_kernel<DP, W, REP, false>), dim3((unsigned)nblocks), dim3(256), lds, s, a);
+    if (a.pair_mode == GPSIG_PAIRS_DIAG || MODE == 1)
+      hipLaunchKernelGGL((pde_adj_kernel<DP, W, REP, false, MODE>), dim3((unsigned)nblocks), dim3(256), lds, s, a);
     else
-      hipLaunchKernelGGL((pde_adj_kernel<DP, W, REP, true>), dim3((unsigned)nblocks), dim3(256), lds, s, a);
+      hipLaunchKernelGGL((pde_adj_kernel<DP, W, REP, true, MODE>), dim3((unsigned)nblocks), dim3(256), lds, s, a);
     return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
   }
 }
 
-template <int DP, int REP>
+template <int DP, int REP, int MODE>
 static int pde_adj_w(const PdeBwdArgs &a, long long nblocks, int W, hipStream_t s) {
   switch (W) {
-    case 1: return launch_pde_adj<DP, 1, REP>(a, nblocks, s);
-    case 2: return launch_pde_adj<DP, 2, REP>(a, nblocks, s);
-    case 4: return launch_pde_adj<DP, 4, REP>(a, nblocks, s);
-    case 8: return launch_pde_adj<DP, 8, REP>(a, nblocks, s);
-    case 16: return launch_pde_adj<DP, 16, REP>(a, nblocks, s);
+    case 1: return launch_pde_adj<DP, 1, REP, MODE>(a, nblocks, s);
+    case 2: return launch_pde_adj<DP, 2, REP, MODE>(a, nblocks, s);
+    case 4: return launch_pde_adj<DP, 4, REP, MODE>(a, nblocks, s);
+    case 8: return launch_pde_adj<DP, 8, REP, MODE>(a, nblocks, s);
+    case 16: return launch_pde_adj<DP, 16, REP, MODE>(a, nblocks, s);
     default: return GPSIG_EUNSUPPORTED;
   }
 }
 
-// one channel count (pde_bwd_inst.hip, one unit per DP)
-template <int DP>
-int pde_bwd_launch_dp(const PdeBwdArgs &a, long long nblocks, hipStream_t s) {
+template <int DP, int MODE>
+static int pde_adj_rep(const PdeBwdArgs &a, long long nblocks, hipStream_t s) {
   const int rep = 1 << a.dyadic;
   const int W = pde_bwd_cols(rep * (a.l2 - 1), rep);
   switch (a.dyadic) {
-    case 0: return pde_adj_w<DP, 1>(a, nblocks, W, s);
-    case 1: return pde_adj_w<DP, 2>(a, nblocks, W, s);
-    case 2: return pde_adj_w<DP, 4>(a, nblocks, W, s);
-    case 3: return pde_adj_w<DP, 8>(a, nblocks, W, s);
+    case 0: return pde_adj_w<DP, 1, MODE>(a, nblocks, W, s);
+    case 1: return pde_adj_w<DP, 2, MODE>(a, nblocks, W, s);
+    case 2: return pde_adj_w<DP, 4, MODE>(a, nblocks, W, s);
+    case 3: return pde_adj_w<DP, 8, MODE>(a, nblocks, W, s);
     default: return GPSIG_EUNSUPPORTED;
+  }
+}
+
+// one channel count (pde_bwd_inst.hip, one unit per DP); mode as pde_adj_kernel's MODE
+template <int DP>
+int pde_bwd_launch_dp(const PdeBwdArgs &a, long long nblocks, int mode, hipStream_t s) {
+  switch (mode) {
+    case 0: return pde_adj_rep<DP, 0>(a, nblocks, s);
+    case 1: return pde_adj_rep<DP, 1>(a, nblocks, s);
+    case 2: return pde_adj_rep<DP, 2>(a, nblocks, s);
+    default: return GPSIG_EINVAL;
   }
 }
 

@@ -5,5 +5,5 @@
 #error "GPSIG_DP must be defined"
 #endif
 namespace gpsig {
-template int pde_bwd_launch_dp<GPSIG_DP>(const PdeBwdArgs &, long long, hipStream_t);
+template int pde_bwd_launch_dp<GPSIG_DP>(const PdeBwdArgs &, long long, int, hipStream_t);
 }

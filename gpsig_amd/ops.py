@@ -235,7 +235,7 @@ def pde_gram(X: torch.Tensor, Y: torch.Tensor | None = None, dyadic: int = 0, so
     return out
 
 
-PDE_VJP_SCRATCH = 4 << 30  # bytes of fp64 K_rev grids per launch (rows are chunked to fit)
+PDE_VJP_SCRATCH = 4 << 30  # bytes of adjoint fronts per launch (rows are chunked to fit)
 
 
 def pde_diag_vjp(X: torch.Tensor, gout: torch.Tensor, dyadic: int = 0, solver: int = 1,
@@ -280,6 +280,59 @@ def pde_gram_vjp(X: torch.Tensor, Y: torch.Tensor | None, gout: torch.Tensor, dy
                                gout.data_ptr(), gX.data_ptr(), gY.data_ptr(), ws.data_ptr(), ws.numel(),
                                _stream(X.device))
         L.check(rc, "gpsig_pde_vjp")
+    return gX, (None if sym else gY)
+
+
+def pde_fronts_bytes(n_pairs: int, l1: int, l2: int, dyadic: int) -> int:
+    """Bytes of the PDE adjoint's forward fronts for n_pairs pairs (0: the adjoint does not apply)."""
+    return int(L.load().gpsig_pde_vjp_workspace_bytes(n_pairs, l1, l2, dyadic))
+
+
+def pde_fronts(X: torch.Tensor, Y: torch.Tensor | None, dyadic: int, solver: int, fronts: torch.Tensor,
+               diag: bool = False) -> torch.Tensor:
+    """Forward of a training step (gpsig_pde_fronts): the values of pde_gram(X, Y) (all n1 x n2 pairs;
+    Y None: Y = X, symmetrised) or, diag=True, of pde_diag(X), and the adjoint's fronts in `fronts` (a
+    float32 buffer of pde_fronts_bytes(...) / 4 elements) for pde_vjp_fronts."""
+    _require_cuda(X, Y, fronts)
+    lib = L.load()
+    X = _f32(X)
+    sym = Y is None
+    Y = X if sym else _f32(Y)
+    n1, l1, d = X.shape
+    n2, l2, _ = Y.shape
+    npairs = n1 if diag else n1 * n2
+    if fronts.dtype != torch.float32 or not fronts.is_contiguous() or fronts.numel() * 4 < pde_fronts_bytes(npairs, l1, l2, dyadic):
+        raise ValueError("fronts must be a contiguous float32 buffer of pde_fronts_bytes() bytes")
+    out = torch.empty((n1,) if diag else (n1, n2), dtype=torch.float32, device=X.device)
+    rc = lib.gpsig_pde_fronts(X.data_ptr(), n1, l1, Y.data_ptr(), n2, l2, d, dyadic, solver,
+                              L.PAIRS_DIAG if diag else L.PAIRS_RECT, 0, n1, out.data_ptr(), fronts.data_ptr(),
+                              fronts.numel() * 4, _stream(X.device))
+    L.check(rc, "gpsig_pde_fronts")
+    if sym and not diag:  # k(x_a, x_b) = k(x_b, x_a): the upper triangle mirrored, as pde_gram's
+        out = torch.triu(out) + torch.triu(out, 1).T
+    return out
+
+
+def pde_vjp_fronts(X: torch.Tensor, Y: torch.Tensor | None, gout: torch.Tensor, dyadic: int, solver: int,
+                   fronts: torch.Tensor, diag: bool = False):
+    """The adjoint from the fronts a pde_fronts call on the same inputs left (gpsig_pde_vjp_fronts):
+    (gX, gY) as pde_gram_vjp, or gX as pde_diag_vjp with diag=True."""
+    _require_cuda(X, Y, gout, fronts)
+    lib = L.load()
+    X, gout = _f32(X), _f32(gout)
+    sym = Y is None
+    Y = X if sym else _f32(Y)
+    n1, l1, d = X.shape
+    n2, l2, _ = Y.shape
+    gX = torch.zeros((n1, l1, d), dtype=torch.float32, device=X.device)
+    gY = gX if (sym or diag) else torch.zeros((n2, l2, d), dtype=torch.float32, device=X.device)
+    rc = lib.gpsig_pde_vjp_fronts(X.data_ptr(), n1, l1, Y.data_ptr(), n2, l2, d, dyadic, solver,
+                                  L.PAIRS_DIAG if diag else L.PAIRS_RECT, 0, n1, gout.data_ptr(), gX.data_ptr(),
+                                  None if diag else gY.data_ptr(), fronts.data_ptr(), fronts.numel() * 4,
+                                  _stream(X.device))
+    L.check(rc, "gpsig_pde_vjp_fronts")
+    if diag:
+        return gX
     return gX, (None if sym else gY)
 
 

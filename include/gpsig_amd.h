@@ -233,6 +233,19 @@ int gpsig_pde_vjp(const float *X, int n1, int l1, const float *Y, int n2, int l2
                   int pair_mode, int row_begin, int row_end, const float *gout, float *gX, float *gY, void *workspace,
                   size_t workspace_bytes, gpsig_stream_t stream);
 
+/* The forward of a training step split off gpsig_pde_vjp: gpsig_pde_fronts evaluates k(x_a, y_b) of the
+ * pairs (pair_mode RECT: out[(a - row_begin) * n2 + b]; DIAG: out[a - row_begin]; the values of
+ * gpsig_pde_gram / gpsig_pde_diag, same cells) and leaves the adjoint's forward fronts in `fronts`
+ * (gpsig_pde_vjp_workspace_bytes(pairs, l1, l2, dyadic) bytes); gpsig_pde_vjp_fronts on the same inputs
+ * and rows then runs only the adjoint's backward sweeps (one solve of the grid fewer than gpsig_pde_vjp). */
+int gpsig_pde_fronts(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int dyadic, int solver,
+                     int pair_mode, int row_begin, int row_end, float *out, void *fronts, size_t fronts_bytes,
+                     gpsig_stream_t stream);
+
+int gpsig_pde_vjp_fronts(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int dyadic,
+                         int solver, int pair_mode, int row_begin, int row_end, const float *gout, float *gX,
+                         float *gY, const void *fronts, size_t fronts_bytes, gpsig_stream_t stream);
+
 /* ---------------------------------------------------------------------------------------------
  * Truncated signatures (replaces iisignature.sig behind iisignature_tensorflow.Sig,
  * gpsig/iisignature_tensorflow.py:87, used by the VOSF Kuf, gpsig/inducing_variables_vosf.py:120-146).

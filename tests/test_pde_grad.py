@@ -115,3 +115,37 @@ def test_pde_cross_vjp_wide_grids(l2, n):
             ry[b] += G[a, b] * gy
     assert norm_rel_err(gX.cpu().numpy(), rx) < 1e-5
     assert norm_rel_err(gY.cpu().numpy(), ry) < 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,solver", [(0, 1), (1, 1), (1, 0), (2, 1)])
+def test_pde_fronts_forward_and_vjp(n, solver):
+    """The training step's split adjoint: gpsig_pde_fronts returns gpsig_pde_gram's / gpsig_pde_diag's
+    values (same cells) and leaves the forward fronts; gpsig_pde_vjp_fronts from them equals gpsig_pde_vjp.
+    Also through autograd (UntruncSignatureKernel.K / Kdiag take this path when a gradient is needed)."""
+    import gpsig_amd
+    from gpsig_amd import ops
+    rng = np.random.default_rng(60 + n)
+    X = torch.tensor(np.cumsum(rng.standard_normal((6, 13, 3)), 1) * 0.3, device=DEV, dtype=torch.float32)
+    Y = torch.tensor(np.cumsum(rng.standard_normal((5, 11, 3)), 1) * 0.3, device=DEV, dtype=torch.float32)
+    G = torch.randn(6, 5, device=DEV)
+    fr = torch.empty(ops.pde_fronts_bytes(30, 13, 11, n) // 4, device=DEV)
+    K = ops.pde_fronts(X, Y, n, solver, fr)
+    torch.testing.assert_close(K, ops.pde_gram(X, Y, n, solver), rtol=0, atol=0)
+    gX, gY = ops.pde_vjp_fronts(X, Y, G, n, solver, fr)
+    rX, rY = ops.pde_gram_vjp(X, Y, G, n, solver)
+    assert norm_rel_err(gX.cpu().numpy(), rX.cpu().numpy()) < 1e-6
+    assert norm_rel_err(gY.cpu().numpy(), rY.cpu().numpy()) < 1e-6
+    w = torch.randn(6, device=DEV)
+    frd = torch.empty(ops.pde_fronts_bytes(6, 13, 13, n) // 4, device=DEV)
+    kd = ops.pde_fronts(X, None, n, solver, frd, diag=True)
+    torch.testing.assert_close(kd, ops.pde_diag(X, n, solver), rtol=0, atol=0)
+    gd = ops.pde_vjp_fronts(X, None, w, n, solver, frd, diag=True)
+    assert norm_rel_err(gd.cpu().numpy(), ops.pde_diag_vjp(X, w, n, solver).cpu().numpy()) < 1e-6
+    # autograd: symmetric K(X) with a gradient (fronts path) vs without (forward only)
+    kp = gpsig_amd.UntruncSignatureKernel(13 * 3, 3, order=n)
+    kp.solver = solver
+    Xf = X.reshape(6, -1).double().requires_grad_(True)
+    Kg = kp.K(Xf)
+    torch.testing.assert_close(Kg.detach(), kp.K(Xf.detach()), rtol=1e-7, atol=0)
+    assert torch.equal(Kg, Kg.T)
