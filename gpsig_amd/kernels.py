@@ -159,7 +159,7 @@ class SignatureKernel:
         if not presliced:
             X, _ = self._slice(X)
         N = X.shape[0]
-        X = X.reshape(N, -1, self.num_features)
+        X = X.reshape(N, int(np.prod(X.shape[1:])) // self.num_features, self.num_features)  # (N = 0 allowed)
         return self._apply_scaling_and_lags_to_sequences(X)
 
     def _scale_vec(self, device):

@@ -100,7 +100,7 @@ class UntruncSignatureKernel:
     def _prep(self, X):
         X = _as_tensor(X)
         N = X.shape[0]
-        return self._apply_scaling_and_lags_to_sequences(X.reshape(N, -1, self.num_features))
+        return self._apply_scaling_and_lags_to_sequences(X.reshape(N, int(np.prod(X.shape[1:])) // self.num_features, self.num_features))
 
     def _dt(self, X):
         return X.dtype if (isinstance(X, torch.Tensor) and X.is_floating_point()) else torch.float64

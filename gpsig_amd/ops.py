@@ -72,6 +72,8 @@ def sig_diag(X: torch.Tensor, num_levels: int, order: int = 1, base="rbf", diffe
     X = _f32(X)
     n, l, d = X.shape
     out = torch.empty((num_levels + 1, n), dtype=torch.float32, device=X.device)
+    if n == 0:  # an empty batch: empty output, as the reference's graph
+        return out
     nb = lib.gpsig_sig_workspace_bytes(n, l, n, l, d)
     ws = workspace(X.device, nb)
     rc = lib.gpsig_sig_diag(X.data_ptr(), n, l, d, num_levels, order, base_kind(base), int(difference), float(jitter),
@@ -110,6 +112,8 @@ def sig_gram(X: torch.Tensor, Y: torch.Tensor | None, num_levels: int, order: in
         shape = (nrows, n2) if out_mode == L.OUT_NORM_SUM else (num_levels + 1, nrows, n2)
         out = torch.empty(shape, dtype=torch.float32, device=X.device)
     out_rows = out.shape[-2]
+    if n1 == 0 or n2 == 0 or r1 == r0:  # an empty batch
+        return out
     if rs1 is not None:
         rs1, rs2 = _f32(rs1), _f32(rs2)
     if scale is not None:
@@ -209,6 +213,8 @@ def pde_diag(X: torch.Tensor, dyadic: int = 0, solver: int = 1) -> torch.Tensor:
     X = _f32(X)
     n, l, d = X.shape
     out = torch.empty((n,), dtype=torch.float32, device=X.device)
+    if n == 0:
+        return out
     L.check(lib.gpsig_pde_diag(X.data_ptr(), n, l, d, dyadic, solver, out.data_ptr(), _stream(X.device)),
             "gpsig_pde_diag")
     return out
@@ -228,6 +234,8 @@ def pde_gram(X: torch.Tensor, Y: torch.Tensor | None = None, dyadic: int = 0, so
         out_row0 = r0
     if out is None:
         out = torch.empty((r1 - out_row0, n2), dtype=torch.float32, device=X.device)
+    if n1 == 0 or n2 == 0 or r1 == r0:
+        return out
     rc = lib.gpsig_pde_gram(X.data_ptr(), n1, l1, Y.data_ptr(), n2, l2, d, dyadic, solver,
                             L.PAIRS_UPPER if sym else L.PAIRS_RECT, r0, r1, out.data_ptr(), out_row0, out.shape[-2],
                             _stream(X.device))
@@ -384,6 +392,8 @@ def signature(X: torch.Tensor, depth: int) -> torch.Tensor:
     X = _f32(X)
     n, l, d = X.shape
     out = torch.empty((n, int(lib.gpsig_signature_channels(d, depth))), dtype=torch.float32, device=X.device)
+    if n == 0:
+        return out
     L.check(lib.gpsig_signature(X.data_ptr(), n, l, d, depth, out.data_ptr(), _stream(X.device)), "gpsig_signature")
     return out
 
@@ -436,6 +446,8 @@ def tens_vs_seq(Z: torch.Tensor, X: torch.Tensor, num_levels: int, order: int = 
     if lt != num_levels * (num_levels + 1) // 2:
         raise ValueError(f"Z must have num_levels*(num_levels+1)/2 = {num_levels * (num_levels + 1) // 2} components")
     out = torch.empty((num_levels + 1, t, n), dtype=torch.float32, device=X.device)
+    if n == 0 or t == 0:
+        return (out, None) if state is not None else out
     ws = workspace(X.device, lib.gpsig_tens_workspace_bytes(n, l, d, lt, t))
     if state is not None:
         if state.dtype != torch.float32 or not state.is_contiguous() or state.numel() < t * n * lt:

@@ -224,3 +224,30 @@ def test_split_diagnostic_matches_fused(N, L, D, M):
         ref = ops.sig_gram(X, Yt, M, base=Lb.BASE_RBF)
         got = ops.sig_gram(X, Yt, M, base=Lb.BASE_RBF | Lb.GRAM_SPLIT)
         torch.testing.assert_close(got, ref, rtol=0, atol=1e-6 * float(ref.abs().max()))
+
+
+def test_empty_and_single_sequence_batches():
+    """Edge batches: no sequences (empty outputs of the right shapes, as the reference's graph), one
+    sequence, one increment (L = 2), a constant path (zero increments: only level 0 survives)."""
+    import gpsig_amd
+    L, D, M = 12, 3, 4
+    k = gpsig_amd.SignatureRBF(L * D, D, M)
+    kp = gpsig_amd.UntruncSignatureKernel(L * D, D, order=1)
+    E = torch.zeros((0, L * D), device=DEV, dtype=torch.float64)
+    X1 = torch.as_tensor(np.cumsum(np.random.default_rng(3).standard_normal((1, L, D)), 1).reshape(1, -1) * 0.2,
+                         device=DEV)
+    assert k.K(E).shape == (0, 0) and k.Kdiag(E).shape == (0,)
+    assert k.K(E, X1).shape == (0, 1) and k.K(X1, E).shape == (1, 0)
+    assert kp.Kdiag(E).shape == (0,) and kp.K(E).shape == (0, 0)
+    Z = torch.zeros((M * (M + 1) // 2, 2, D), device=DEV, dtype=torch.float64)
+    assert k.K_tens_vs_seq(Z, E).shape == (2, 0)
+    ref = kr.SignatureKernelRef(L * D, D, M)
+    np.testing.assert_allclose(k.K(X1).cpu().numpy(), ref.K(X1.cpu().numpy()), rtol=1e-5)
+    # one increment and a constant path
+    for X in (np.random.default_rng(4).standard_normal((3, 2, D)) * 0.3, np.ones((2, 5, D))):
+        n, l, _ = X.shape
+        kk = gpsig_amd.SignatureRBF(l * D, D, M, normalization=False)
+        rr = kr.SignatureKernelRef(l * D, D, M, normalization=False)
+        got = kk.K(torch.as_tensor(X.reshape(n, -1), device=DEV), return_levels=True).cpu().numpy()
+        exp = rr.K(X.reshape(n, -1), return_levels=True)
+        np.testing.assert_allclose(got, exp, rtol=1e-5, atol=1e-6)
