@@ -36,24 +36,26 @@ struct TvsBwdArgs {
                       // the forward sweep is skipped
 };
 
-// Level I only (levels are independent chains; blockIdx.z selects the level, so the per-lane state is
-// O(I * DP) and not O(M^2 * DP)).  LT below is the number of components of this level.
-// DIFF = false (difference=False): the cells are the point values P_k(s) themselves, s = 0..L-1.
 // waves (tensors) per workgroup of the VJP
 template <int DP, bool INCR>
 constexpr int tvs_bwd_waves() { return (DP <= 6 && !INCR) ? 8 : 4; }
-// time steps per staged chunk of the sequence records (x, dx, g of the workgroup's 64 sequences)
-#ifndef GPSIG_TVSB_CS
-#define GPSIG_TVSB_CS 8
-#endif
-template <int DP>
-constexpr int tvs_bwd_chunk() { return DP <= 8 ? GPSIG_TVSB_CS : 2; }
+// time steps per staged chunk of the sequence records (x, dx, g of the workgroup's 64 sequences): 4 keeps
+// the 8-wave workgroups at two per CU (4 waves/SIMD); the register-bound increments variants (one wave
+// per SIMD) take 8 steps of prefetch distance
+template <int DP, bool INCR>
+constexpr int tvs_bwd_chunk() { return DP > 8 ? 2 : (INCR ? 8 : 4); }
 
+// reverse-sweep steps between exact point values of the RBF difference cells (backward recurrence)
+constexpr int TVSB_ANCHOR = 8;
+
+// Level I only (levels are independent chains; blockIdx.z selects the level, so the per-lane state is
+// O(I * DP) and not O(M^2 * DP)).  LT below is the number of components of this level.
+// DIFF = false (difference=False): the cells are the point values P_k(s) themselves, s = 0..L-1.
 template <int DP, int I, int MMAX, bool INCR, bool RBF, bool DIFF>
 __device__ __forceinline__ void tvs_bwd_level(const TvsBwdArgs &a,
                                               float (&zl_all)[tvs_bwd_waves<DP, INCR>()][MMAX * 2 * DP],
                                               float (&red)[2][tvs_bwd_waves<DP, INCR>()][DP][64],
-                                              float (&stg)[2][tvs_bwd_chunk<DP>() + 1][2 * DP + 1][64]) {
+                                              float (&stg)[2][tvs_bwd_chunk<DP, INCR>() + 1][2 * DP + 1][64]) {
   constexpr int LT = I;
   constexpr int NW = tvs_bwd_waves<DP, INCR>();
   constexpr int KB = I * (I - 1) / 2;  // first component of the level
@@ -88,7 +90,7 @@ __device__ __forceinline__ void tvs_bwd_level(const TvsBwdArgs &a,
   // each (step, channel) row of 64 floats is fetched once per workgroup by one global_load_lds (an
   // LDS-DMA, no registers), a chunk of CS steps ahead of its use.  stg[buf][step - c0][slot][lane]:
   // slots 0..DP-1 = x, DP..2DP-1 = dx, 2DP = g (padded channels are zeroed once, never loaded).
-  constexpr int CS = tvs_bwd_chunk<DP>();
+  constexpr int CS = tvs_bwd_chunk<DP, INCR>();
   const int NCH = 2 * d + 1;
   for (int e = (int)threadIdx.x; e < 2 * (CS + 1) * 2 * DP * 64; e += NW * 64) {
     const int l = e & 63, r = e >> 6, slot = r % (2 * DP), si = (r / (2 * DP)) % (CS + 1), b = r / (2 * DP * (CS + 1));
@@ -348,11 +350,26 @@ __device__ __forceinline__ void tvs_bwd_level(const TvsBwdArgs &a,
     {
       constexpr int i = I, k0 = 0;
       float m[I], Av[I];
+      // RBF difference cells without increments: k(z, x_s) = k(z, x_{s+1}) / (1 + expm1(q_s)) from the cell's
+      // own expm1 (no exp, no distance), re-anchored exactly every TVSB_ANCHOR steps (wave-uniform)
+      constexpr bool BACKREC = RBF && DIFF && !INCR;
+      const bool anchor = !BACKREC || (s % TVSB_ANCHOR) == 0 || s == stop;
 #pragma unroll
       for (int st = 0; st < i; ++st) {
         const int k = k0 + st;
-        pvals(k, x, c0v[k], c1v[k]);
-        m[st] = DIFF ? cell(k, x, dx, gs, c0v[k], c1v[k], pv0[k], pv1[k]) : pcell(k, x, c0v[k], c1v[k]);
+        if constexpr (BACKREC) {
+          float qv = -gs;
+#pragma unroll
+          for (int q = 0; q < DP; ++q) qv = __builtin_fmaf(z0c(k, q), dx[q], qv);
+          const float E = em1(qv);
+          if (anchor) pvals(k, x, c0v[k], c1v[k]);
+          else c0v[k] = pv0[k] * __builtin_amdgcn_rcpf(1.0f + E);
+          c1v[k] = 0.f;
+          m[st] = c0v[k] * E;
+        } else {
+          pvals(k, x, c0v[k], c1v[k]);
+          m[st] = DIFF ? cell(k, x, dx, gs, c0v[k], c1v[k], pv0[k], pv1[k]) : pcell(k, x, c0v[k], c1v[k]);
+        }
       }
       // A_j(s) = A_j(s+1) - M_{c_j}(s) A_{j-1}(s), ascending j (A_0 = 1)
       Av[0] = 1.0f;
@@ -434,7 +451,7 @@ __global__ __launch_bounds__((64 * tvs_bwd_waves<DP, INCR>())) void tvs_bwd_kern
   constexpr int NW = tvs_bwd_waves<DP, INCR>();
   __shared__ float zl_all[NW][M * 2 * DP];
   __shared__ float red[2][NW][DP][64];
-  __shared__ float stg[2][tvs_bwd_chunk<DP>() + 1][2 * DP + 1][64];
+  __shared__ float stg[2][tvs_bwd_chunk<DP, INCR>() + 1][2 * DP + 1][64];
   switch (blockIdx.z) {
     case 0: tvs_bwd_level<DP, 1, M, INCR, RBF, DIFF>(a, zl_all, red, stg); break;
     case 1: if constexpr (M >= 2) tvs_bwd_level<DP, 2, M, INCR, RBF, DIFF>(a, zl_all, red, stg); break;
