@@ -64,6 +64,33 @@ def base_kind(base) -> int:
 
 
 # ----------------------------------------------------------------------------- truncated kernels
+# The exact signature kernel (linear base kernel, difference=True, order >= num_levels): the higher-order
+# recursion (signature_algs.py:37-74) is then exactly K_m(x, y) = <S_m(x), S_m(y)> (tests/golden/linear_chen.npz
+# pins it), so the Gram is computed as truncated signatures (gpsig_signature) + one GEMM per level on the
+# matrix cores (hipBLASLt fp32) instead of the O(order^2 L^2) recursion per pair -- the configuration the
+# reference's VOSF / exact-signature models train (benchmarks/models/train_gpsig_vosf.py:102,
+# train_gpsig_.py:62).  Up to this many signature coordinates per sequence (the signature kernel's LDS).
+SIG_FEATURE_MAX = 16000
+
+
+def _sig_feature_path(order: int, base, difference: bool, num_levels: int, d: int) -> bool:
+    if order < num_levels or not difference or base_kind(base) != L.BASE_LINEAR:
+        return False
+    return 0 < int(L.load().gpsig_signature_channels(d, num_levels)) <= SIG_FEATURE_MAX
+
+
+def _sig_feature_levels(S1: torch.Tensor, S2: torch.Tensor, d: int, num_levels: int) -> torch.Tensor:
+    """(M+1, n1, n2): level 0 = 1, level m = S_m(x) S_m(y)^T (one fp32 GEMM per level)."""
+    out = torch.empty((num_levels + 1, S1.shape[0], S2.shape[0]), dtype=torch.float32, device=S1.device)
+    out[0] = 1.0
+    off = 0
+    for m in range(1, num_levels + 1):
+        w = d ** m
+        torch.matmul(S1[:, off:off + w], S2[:, off:off + w].T, out=out[m])
+        off += w
+    return out
+
+
 def sig_diag(X: torch.Tensor, num_levels: int, order: int = 1, base="rbf", difference: bool = True,
              jitter: float = 0.0, rsqrt: bool = False) -> torch.Tensor:
     """Per-level k(x_a, x_a), (num_levels+1, n) float32 [rsqrt: 1/sqrt(k + jitter)]."""
@@ -74,6 +101,15 @@ def sig_diag(X: torch.Tensor, num_levels: int, order: int = 1, base="rbf", diffe
     out = torch.empty((num_levels + 1, n), dtype=torch.float32, device=X.device)
     if n == 0:  # an empty batch: empty output, as the reference's graph
         return out
+    if _sig_feature_path(order, base, difference, num_levels, d):
+        S = signature(X, num_levels)
+        out[0] = 1.0
+        off = 0
+        for m in range(1, num_levels + 1):
+            w = d ** m
+            out[m] = (S[:, off:off + w] ** 2).sum(1)
+            off += w
+        return torch.rsqrt(out + float(jitter)) if rsqrt else out
     nb = lib.gpsig_sig_workspace_bytes(n, l, n, l, d)
     ws = workspace(X.device, nb)
     rc = lib.gpsig_sig_diag(X.data_ptr(), n, l, d, num_levels, order, base_kind(base), int(difference), float(jitter),
@@ -113,6 +149,25 @@ def sig_gram(X: torch.Tensor, Y: torch.Tensor | None, num_levels: int, order: in
         out = torch.empty(shape, dtype=torch.float32, device=X.device)
     out_rows = out.shape[-2]
     if n1 == 0 or n2 == 0 or r1 == r0:  # an empty batch
+        return out
+    if state is None and _sig_feature_path(order, base, difference, num_levels, d):
+        # the exact signature kernel: signatures + per-level GEMMs, then the fused epilogue's arithmetic
+        S1 = signature(X[r0:r1], num_levels)
+        S2 = signature(Y, num_levels)
+        K = _sig_feature_levels(S1, S2, d, num_levels)
+        if out_mode != L.OUT_LEVELS:
+            if sym and jitter:
+                idx = torch.arange(r0, r1, device=X.device)
+                K[:, idx - r0, idx] += float(jitter)
+            if rs1 is not None:
+                K = K * _f32(rs1)[:, r0:r1, None] * _f32(rs2)[:, None, :]
+            if scale is not None:
+                K = K * _f32(scale)[:, None, None]
+        if out_mode == L.OUT_NORM_SUM:
+            K = K.sum(0)
+        out[..., r0 - out_row0:r1 - out_row0, :] = K
+        if sym and rows is None:  # k(x_a, x_b) = k(x_b, x_a) exactly, as the mirrored kernel output
+            out.copy_(torch.triu(out) + torch.triu(out, 1).transpose(-1, -2))
         return out
     if rs1 is not None:
         rs1, rs2 = _f32(rs1), _f32(rs2)

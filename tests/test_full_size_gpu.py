@@ -114,7 +114,9 @@ def test_vosf_kuf_full_size_C4():
     S = np.unique(np.linspace(0, N - 1, 12).astype(int))
     St = torch.as_tensor(S, device=DEV)
     _, Kzx_s, _ = feat.Kuu_Kuf_Kff(k, Xt[St])
-    torch.testing.assert_close(Kzx[:, St], Kzx_s, rtol=0, atol=0)
+    # per-sequence independence; the exact signature kernel's norms (the feature path: signatures and a
+    # library reduction per level, ops._sig_feature_path) sum in a batch-size dependent order
+    torch.testing.assert_close(Kzx[:, St], Kzx_s, rtol=1e-6, atol=0)
     slv = sg.compute_trunc(Mz, D)
     assert slv == 4
     Xs = X[S].astype(np.float64)

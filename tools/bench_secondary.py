@@ -40,6 +40,14 @@ res["gram_lin_o1_N1024_L100_M5_ms"] = timed(lambda: ops.sig_gram(X, None, 5, bas
 res["gram_rbf_o2_N1024_L100_M5_ms"] = timed(lambda: ops.sig_gram(X, None, 5, order=2))
 Xs = walks(256, 64, 4)
 res["gram_lin_oM_N256_L64_M5_ms"] = timed(lambda: ops.sig_gram(Xs, None, 5, order=5, base="linear"))
+# the exact signature kernel at the reference's VOSF training shape (max_len 500 is the data's; L=100 here):
+# signature features + per-level GEMMs vs the higher-order recursion (order = num_levels - 1 forces it)
+Xv = walks(1024, 100, 5)
+res["gram_lin_oM_N1024_L100_D5_M4_features_ms"] = timed(lambda: ops.sig_gram(Xv, None, 4, order=4, base="linear"))
+ops_max = ops.SIG_FEATURE_MAX
+ops.SIG_FEATURE_MAX = 0
+res["gram_lin_oM_N1024_L100_D5_M4_recursion_ms"] = timed(lambda: ops.sig_gram(Xv, None, 4, order=4, base="linear"))
+ops.SIG_FEATURE_MAX = ops_max
 Xp = walks(512, 100, 5)
 for dy in (0, 2):
     res[f"pde_gram_N512_L100_dyadic{dy}_ms"] = timed(lambda: ops.pde_gram(Xp, None, dy, 1))
