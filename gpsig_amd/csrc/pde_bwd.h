@@ -41,6 +41,7 @@ struct PdeBwdArgs {
   int dyadic, solver;
   int pair_mode, row_begin, row_end;
   int ntb, tiles_a0;
+  int wpb;            // waves (pairs) per workgroup: 4, or 2 / 1 when the per-wave LDS of long x needs it
   const float *gout;  // DIAG: (n1,); RECT: (n1, n2)
   float *gX, *gY;     // accumulated (n1, l1, d), (n2, l2, d)
   float *fronts;      // workspace: per evaluated pair, nfronts x (W + REP) x 64 floats (pde_front_floats)
@@ -54,45 +55,77 @@ GPSIG_DEV double lane_next_d(double v) { return dpp_d<0x130>(v); }
 template <int W, int REP>
 constexpr int pde_chunk() { return REP * W >= 32 ? 1 : 32 / (REP * W); }
 
-// Columns per lane of the adjoint kernel: the smallest power of two >= REP with ceil(J / W) <= 64 lanes
-// (J <= 1024 fine columns); 0 when unsupported.
+// Columns per lane of the adjoint kernel: the smallest power of two >= REP with ceil(J / W) <= 64 lanes,
+// else the widest the registers take (REP * W <= 64, W <= 16) and the grid is swept in column blocks of
+// 64 W fine columns; 0 when unsupported (REP > 8).
 __host__ __device__ inline int pde_bwd_cols(int J, int rep) {
-  for (int W = 1; W <= 16; W *= 2)
-    if (W >= rep && (long long)64 * W >= J) return (rep * W <= 64) ? W : 0;
-  return 0;
+  if (rep > 8) return 0;
+  const int wmax = rep * 16 <= 64 ? 16 : 64 / rep;
+  for (int W = rep; W <= wmax; W *= 2)
+    if ((long long)64 * W >= J) return W;
+  return wmax;
 }
-// fp32 words of the stored K fronts of one pair
-inline long long pde_front_floats(int l1, int l2, int dyadic) {
-  if (dyadic < 0 || dyadic > 4) return 0;
+
+// Per-pair workspace of the adjoint: the K fronts of every column block, then (several blocks only)
+// fp64 boundary columns [nblk][I + 1]: slot b >= 1 the K values entering block b from the left, slot 0
+// the R values entering a block from the right (reused in place, block by block).
+struct PdeLayout {
+  int W, H, nblk, nfr;     // nfr: fronts per block
+  long long kb_off;        // float offset of the boundary columns
+  long long pair_floats;   // fp32 words per pair (a multiple of 2)
+};
+__host__ __device__ inline PdeLayout pde_layout(int l1, int l2, int dyadic) {
+  PdeLayout L{};
+  if (dyadic < 0 || dyadic > 3 || l1 < 2 || l2 < 2) return L;
   const int rep = 1 << dyadic;
-  const long long JL = (long long)(l2 - 1) * rep;
-  if (JL > 1024) return 0;
+  const long long IC = l1 - 1, JL = (long long)(l2 - 1) * rep;
+  if (JL > (1LL << 30)) return L;
   const int J = (int)JL, W = pde_bwd_cols(J, rep);
-  if (W == 0) return 0;
-  const long long H = rep * W >= 32 ? 1 : 32 / (rep * W), U = (J + W - 1) / W;
-  const long long nfr = ((l1 - 1) + U - 1 + H - 1) / H;
-  return nfr * (W + rep) * 64;
+  if (W == 0) return L;
+  L.W = W;
+  L.H = rep * W >= 32 ? 1 : 32 / (rep * W);
+  const long long CB = 64LL * W;
+  L.nblk = (int)((J + CB - 1) / CB);
+  const long long U = L.nblk == 1 ? (J + W - 1) / W : 64;
+  L.nfr = (int)((IC + U - 1 + L.H - 1) / L.H);
+  L.kb_off = (long long)L.nblk * L.nfr * (W + rep) * 64;
+  L.pair_floats = L.kb_off + (L.nblk > 1 ? 2LL * L.nblk * (IC * rep + 1) : 0);
+  return L;
 }
+// fp32 words of the adjoint's workspace for one pair (0: unsupported)
+inline long long pde_front_floats(int l1, int l2, int dyadic) { return pde_layout(l1, l2, dyadic).pair_floats; }
+
+// LDS of one wave (pair) of the adjoint kernel, in doubles
+__host__ __device__ inline size_t pde_lds_wave_doubles(int IC, int DP) { return ((size_t)IC * DP * 12 + 7) / 8; }
+
+GPSIG_DEV double ld_l2_d(const double *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
 // MODE 0: both passes (gpsig_pde_vjp); 1: pass A only, plus the kernel value K[I][J] of every pair (the
 // forward of a training step, gpsig_pde_fronts); 2: pass B only, from the fronts a MODE 1 launch left
 // (gpsig_pde_vjp_fronts).
+// Column blocks (J > 64 W): pass A sweeps the blocks left to right, the wave's lane 63 handing its right
+// column of K to the next block through the workspace (lane 0 of that block reads it as its left
+// boundary: pde_rep_kernel's slab, in HBM since pass B re-reads it); pass B sweeps them right to left,
+// lane 0 handing its left column of R to the next block the same way (lane 63's right boundary).  The
+// cells, recurrences and summation order within a cell are those of one block, so the result does not
+// depend on the blocking beyond the order of the per-row atomics.
 template <int DP, int W, int REP, bool COLS, int MODE = 0>
 __global__ __launch_bounds__(256) void pde_adj_kernel(PdeBwdArgs p) {
   static_assert(W % REP == 0, "a lane owns whole coarse columns");
   constexpr int WC = W / REP;
   constexpr int H = pde_chunk<W, REP>();
   constexpr int FW = W + REP;  // front words per lane: up[W], last[0 .. REP-2], corner_prev
+  constexpr int CB = 64 * W;   // fine columns per block
   extern __shared__ __attribute__((aligned(16))) double ldsd[];
   const int lane = threadIdx.x & 63;
   const int wave = wave_uniform(threadIdx.x >> 6);
   const bool diag = p.pair_mode == GPSIG_PAIRS_DIAG;
   int a, b;
   if (diag) {
-    a = p.row_begin + (int)blockIdx.x * 4 + wave;
+    a = p.row_begin + (int)blockIdx.x * p.wpb + wave;
     b = a;
   } else {
-    a = (p.tiles_a0 + (int)blockIdx.x / p.ntb) * 4 + wave;
+    a = (p.tiles_a0 + (int)blockIdx.x / p.ntb) * p.wpb + wave;
     b = (int)blockIdx.x % p.ntb;
   }
   const bool ok = a >= p.row_begin && a < p.row_end && b < p.n2;  // wave-uniform
@@ -100,20 +133,19 @@ __global__ __launch_bounds__(256) void pde_adj_kernel(PdeBwdArgs p) {
 
   const double inv_factor = 1.0 / (double)(REP * REP);
   const int IC = p.l1 - 1, JC = p.l2 - 1;
-  const int J = JC * REP;
+  const int J = JC * REP, I = IC * REP;
   const int d = p.d;
   const float *x = p.X + (long long)a * p.l1 * d;
   const float *y = p.Y + (long long)b * p.l2 * d;
   const long long pidx = diag ? (long long)(a - p.row_begin) : (long long)(a - p.row_begin) * p.n2 + b;
-  const int U = (J + W - 1) / W;
-  const int nsteps = IC + U - 1;
-  const int nfr = (nsteps + H - 1) / H;
-  float *__restrict__ fr = p.fronts + pidx * (long long)nfr * FW * 64;
+  const PdeLayout lay = pde_layout(p.l1, p.l2, p.dyadic);
+  const int nblk = lay.nblk;
+  float *__restrict__ fr = p.fronts + pidx * lay.pair_floats;
+  double *kbr = reinterpret_cast<double *>(fr + lay.kb_off);
 
-  // LDS: [wave] { dx (IC x DP floats, as doubles' storage) | coarse-row accumulators (IC x DP doubles) }
-  double *wl = ldsd + (size_t)wave * IC * DP * 2;
-  float *dxs = reinterpret_cast<float *>(wl);
-  double *gacc = wl + (size_t)IC * DP;
+  // LDS: [wave] { coarse-row accumulators (IC x DP doubles) | dx (IC x DP floats) }
+  double *gacc = ldsd + (size_t)wave * pde_lds_wave_doubles(IC, DP);
+  float *dxs = reinterpret_cast<float *>(gacc + (size_t)IC * DP);
   for (int r = lane; r < IC; r += 64) {
 #pragma unroll
     for (int k = 0; k < DP; ++k) {
@@ -121,21 +153,27 @@ __global__ __launch_bounds__(256) void pde_adj_kernel(PdeBwdArgs p) {
       gacc[r * DP + k] = 0.0;
     }
   }
-  // y increments of this lane's coarse columns
-  float dy[WC][DP];
-#pragma unroll
-  for (int w = 0; w < WC; ++w) {
-    int cj = lane * WC + w;
-    cj = cj < JC - 1 ? cj : JC - 1;
-#pragma unroll
-    for (int k = 0; k < DP; ++k) dy[w][k] = k < d ? y[(cj + 1) * d + k] - y[cj * d + k] : 0.0f;
-  }
-  double dyd[WC][DP];  // fp64 copies for the contractions (converted once, not per cell)
-#pragma unroll
-  for (int w = 0; w < WC; ++w)
-#pragma unroll
-    for (int k = 0; k < DP; ++k) dyd[w][k] = (double)dy[w][k];
   __syncthreads();
+
+  // the current column block: first fine column, lanes used, y increments of the lane's coarse columns
+  int c0 = 0, U = 0;
+  float dy[WC][DP];
+  double dyd[WC][DP];  // fp64 copies for the contractions (converted once, not per cell)
+  auto load_block = [&](int blk) {
+    c0 = blk * CB;
+    U = (J - c0 + W - 1) / W;
+    U = U < 64 ? U : 64;
+#pragma unroll
+    for (int w = 0; w < WC; ++w) {
+      int cj = c0 / REP + lane * WC + w;
+      cj = cj < JC - 1 ? cj : JC - 1;
+#pragma unroll
+      for (int k = 0; k < DP; ++k) {
+        dy[w][k] = k < d ? y[(cj + 1) * d + k] - y[cj * d + k] : 0.0f;
+        dyd[w][k] = (double)dy[w][k];
+      }
+    }
+  };
 
   const bool s1 = p.solver == 1;
   const bool hybrid = diag && p.solver == 0;
@@ -154,12 +192,24 @@ __global__ __launch_bounds__(256) void pde_adj_kernel(PdeBwdArgs p) {
 
   // ---- K sweep state and one forward step (pde_rep_kernel's scheme); kc[r][w] = K(i, c) of cell (i, c)
   double up[W], last[REP], corner_prev;
+  const double *kin = nullptr;  // the block's left boundary column K(., c0) (null: the boundary 1)
+  auto kinit = [&]() {
+#pragma unroll
+    for (int w = 0; w < W; ++w) up[w] = 1.0;
+#pragma unroll
+    for (int r = 0; r < REP; ++r) last[r] = 1.0;
+    corner_prev = 1.0;
+  };
   auto kstep = [&](int s, float (&kc)[REP][W]) {
     double left[REP];
 #pragma unroll
-    for (int r = 0; r < REP; ++r) {
-      left[r] = lane_prev(last[r]);
-      if (lane == 0) left[r] = 1.0;
+    for (int r = 0; r < REP; ++r) left[r] = lane_prev(last[r]);
+    if (lane == 0) {
+#pragma unroll
+      for (int r = 0; r < REP; ++r) {
+        const int i1 = s * REP + r + 1;
+        left[r] = kin ? ld_l2_d(kin + (i1 < I ? i1 : I)) : 1.0;
+      }
     }
     const int ci = s - lane;
     if (ci >= 0 && ci < IC && lane < U) {
@@ -186,7 +236,7 @@ __global__ __launch_bounds__(256) void pde_adj_kernel(PdeBwdArgs p) {
             kn = (upw + lft) * A[w / REP] - cor * B[w / REP];
           } else {
             kn = (upw + lft) + cor * B[w / REP];
-            if (hybrid && lane * W + w == i) {
+            if (hybrid && c0 + lane * W + w == i) {
               const double t = A[w / REP], t2 = t * t;
               kn = (upw + lft) * (1.0 + 0.5 * t + (1.0 / 12) * t2) - cor * (1.0 - (1.0 / 12) * t2);
             }
@@ -202,30 +252,40 @@ __global__ __launch_bounds__(256) void pde_adj_kernel(PdeBwdArgs p) {
     corner_prev = left[REP - 1];
   };
 
-  // ---- pass A: K forward, a front every H steps (last[REP-1] is up[W-1] after any step)
+  // ---- pass A: K forward block by block, a front every H steps (last[REP-1] is up[W-1] after any step)
+  for (int blk = 0; MODE != 2 && ok && blk < nblk; ++blk) {
+    load_block(blk);
+    kin = blk > 0 ? kbr + (long long)blk * (I + 1) : nullptr;
+    double *kout = blk + 1 < nblk ? kbr + (long long)(blk + 1) * (I + 1) : nullptr;
+    float *fb = fr + (long long)blk * lay.nfr * FW * 64;
+    kinit();
+    const int nsteps = IC + U - 1;
+    for (int s0 = 0; s0 < nsteps; s0 += H) {
+      float *f = fb + (long long)(s0 / H) * FW * 64;
 #pragma unroll
-  for (int w = 0; w < W; ++w) up[w] = 1.0;
+      for (int w = 0; w < W; ++w) f[w * 64 + lane] = (float)up[w];
 #pragma unroll
-  for (int r = 0; r < REP; ++r) last[r] = 1.0;
-  corner_prev = 1.0;
-  const int nst = ok ? nsteps : 0;  // invalid waves still reach the barrier below
-  for (int s0 = 0; MODE != 2 && s0 < nst; s0 += H) {
-    float *f = fr + (long long)(s0 / H) * FW * 64;
+      for (int r = 0; r + 1 < REP; ++r) f[(W + r) * 64 + lane] = (float)last[r];
+      f[(W + REP - 1) * 64 + lane] = (float)corner_prev;
 #pragma unroll
-    for (int w = 0; w < W; ++w) f[w * 64 + lane] = (float)up[w];
+      for (int h = 0; h < H; ++h) {
+        float kc[REP][W];
+        const int s = s0 + h;
+        if (s < nsteps) {
+          kstep(s, kc);
+          const int ci = s - 63;  // lane 63 (a full block) hands its right column on
+          if (kout && lane == 63 && ci >= 0 && ci < IC) {
 #pragma unroll
-    for (int r = 0; r + 1 < REP; ++r) f[(W + r) * 64 + lane] = (float)last[r];
-    f[(W + REP - 1) * 64 + lane] = (float)corner_prev;
-#pragma unroll
-    for (int h = 0; h < H; ++h) {
-      float kc[REP][W];
-      if (s0 + h < nsteps) kstep(s0 + h, kc);
+            for (int r = 0; r < REP; ++r) kout[ci * REP + r + 1] = last[r];
+          }
+        }
+      }
     }
   }
 
   if constexpr (MODE == 1) {
     // K[I][J] = the last row's value in fine column J - 1 (the forward op's value: same cells)
-    const int owner = (J - 1) / W, slot = (J - 1) % W;
+    const int owner = (J - 1 - c0) / W, slot = (J - 1 - c0) % W;
     double res = 0.0;
 #pragma unroll
     for (int w = 0; w < W; ++w)
@@ -236,92 +296,128 @@ __global__ __launch_bounds__(256) void pde_adj_kernel(PdeBwdArgs p) {
     }
     return;
   }
-  // ---- pass B: chunks backwards; the R sweep runs continuously in its own step order
-  double ru[W], rlast[REP], rcorner = 1.0;
+  const float g = diag ? p.gout[a] : p.gout[(long long)a * p.n2 + b];
+  // ---- pass B: blocks right to left, chunks backwards; the R sweep runs in its own step order
+  double ru[W], rlast[REP], rcorner;
   double gcol[WC][DP];
+  for (int blk = nblk - 1; ok && blk >= 0; --blk) {
+    load_block(blk);
+    kin = blk > 0 ? kbr + (long long)blk * (I + 1) : nullptr;
+    const double *rin = blk + 1 < nblk ? kbr : nullptr;  // R(., c0 + CB), left by the block on the right
+    double *rout = blk > 0 ? kbr : nullptr;                // R(., c0), for the block on the left
+    const float *fb = fr + (long long)blk * lay.nfr * FW * 64;
 #pragma unroll
-  for (int w = 0; w < W; ++w) ru[w] = 1.0;
+    for (int w = 0; w < W; ++w) ru[w] = 1.0;
 #pragma unroll
-  for (int r = 0; r < REP; ++r) rlast[r] = 1.0;
+    for (int r = 0; r < REP; ++r) rlast[r] = 1.0;
+    rcorner = 1.0;
 #pragma unroll
-  for (int w = 0; w < WC; ++w)
+    for (int w = 0; w < WC; ++w)
 #pragma unroll
-    for (int k = 0; k < DP; ++k) gcol[w][k] = 0.0;
-  for (int s0 = ((nst - 1) / H) * H; nst > 0 && s0 >= 0; s0 -= H) {
-    const float *f = fr + (long long)(s0 / H) * FW * 64;
+      for (int k = 0; k < DP; ++k) gcol[w][k] = 0.0;
+    const int nsteps = IC + U - 1;
+    for (int s0 = ((nsteps - 1) / H) * H; s0 >= 0; s0 -= H) {
+      const float *f = fb + (long long)(s0 / H) * FW * 64;
 #pragma unroll
-    for (int w = 0; w < W; ++w) up[w] = (double)f[w * 64 + lane];
+      for (int w = 0; w < W; ++w) up[w] = (double)f[w * 64 + lane];
 #pragma unroll
-    for (int r = 0; r + 1 < REP; ++r) last[r] = (double)f[(W + r) * 64 + lane];
-    last[REP - 1] = up[W - 1];
-    corner_prev = (double)f[(W + REP - 1) * 64 + lane];
-    float kc[H][REP][W];
+      for (int r = 0; r + 1 < REP; ++r) last[r] = (double)f[(W + r) * 64 + lane];
+      last[REP - 1] = up[W - 1];
+      corner_prev = (double)f[(W + REP - 1) * 64 + lane];
+      float kc[H][REP][W];
 #pragma unroll
-    for (int h = 0; h < H; ++h)
-      if (s0 + h < nsteps) kstep(s0 + h, kc[h]);
+      for (int h = 0; h < H; ++h)
+        if (s0 + h < nsteps) kstep(s0 + h, kc[h]);
 #pragma unroll
-    for (int h = H - 1; h >= 0; --h) {
-      if (s0 + h >= nsteps) continue;
-      double right[REP];
+      for (int h = H - 1; h >= 0; --h) {
+        if (s0 + h >= nsteps) continue;
+        double right[REP];
 #pragma unroll
-      for (int r = 0; r < REP; ++r) {
-        right[r] = lane_next_d(rlast[r]);
-        if (lane == 63) right[r] = 1.0;
-      }
-      const int ci = s0 + h - lane;
-      if (ci >= 0 && ci < IC && lane < U) {
-        double inc[WC], S[WC];
-        float dxv[DP];
-        incs(ci, inc, dxv);
+        for (int r = 0; r < REP; ++r) right[r] = lane_next_d(rlast[r]);
+        if (lane == 63) {
 #pragma unroll
-        for (int w = 0; w < WC; ++w) {
-          inc[w] -= 1.0;
-          S[w] = 0.0;
-        }
-#pragma unroll
-        for (int r = REP - 1; r >= 0; --r) {
-          double rgt = right[r];
-          double cor = r == REP - 1 ? rcorner : right[r + 1];
-#pragma unroll
-          for (int w = W - 1; w >= 0; --w) {
-            const int c = lane * W + w;
-            const double upw = ru[w];
-            const double rn = (upw + rgt) + cor * inc[w / REP];
-            if (c < J) {  // columns >= J keep the boundary value 1
-              // KK[i][c] = K(i, c) * R(i+1, c+1) = K[i][c] * K_rev[I-1-i][J-1-c]
-              S[w / REP] = __builtin_fma((double)kc[h][r][w], cor, S[w / REP]);
-              cor = upw;
-              rgt = rn;
-              ru[w] = rn;
-            }
+          for (int r = 0; r < REP; ++r) {  // rows at or past I: the boundary 1
+            const int pr = (s0 + h - 63) * REP + r;
+            right[r] = rin && pr < I ? ld_l2_d(rin + (pr > 0 ? pr : 0)) : 1.0;
           }
-          rlast[r] = rgt;
         }
-        double grow[DP], dxd[DP];
+        const int ci = s0 + h - lane;
+        if (ci >= 0 && ci < IC && lane < U) {
+          double inc[WC], S[WC];
+          float dxv[DP];
+          incs(ci, inc, dxv);
 #pragma unroll
-        for (int k = 0; k < DP; ++k) {
-          grow[k] = 0.0;
-          dxd[k] = (double)dxv[k];
-        }
+          for (int w = 0; w < WC; ++w) {
+            inc[w] -= 1.0;
+            S[w] = 0.0;
+          }
 #pragma unroll
-        for (int w = 0; w < WC; ++w)
+          for (int r = REP - 1; r >= 0; --r) {
+            double rgt = right[r];
+            double cor = r == REP - 1 ? rcorner : right[r + 1];
+#pragma unroll
+            for (int w = W - 1; w >= 0; --w) {
+              const int c = c0 + lane * W + w;
+              const double upw = ru[w];
+              const double rn = (upw + rgt) + cor * inc[w / REP];
+              if (c < J) {  // columns >= J keep the boundary value 1
+                // KK[i][c] = K(i, c) * R(i+1, c+1) = K[i][c] * K_rev[I-1-i][J-1-c]
+                S[w / REP] = __builtin_fma((double)kc[h][r][w], cor, S[w / REP]);
+                cor = upw;
+                rgt = rn;
+                ru[w] = rn;
+              }
+            }
+            rlast[r] = rgt;
+          }
+          if (rout && lane == 0) {
+#pragma unroll
+            for (int r = 0; r < REP; ++r) rout[ci * REP + r] = rlast[r];
+          }
+          double grow[DP], dxd[DP];
 #pragma unroll
           for (int k = 0; k < DP; ++k) {
-            grow[k] = __builtin_fma(S[w], dyd[w][k], grow[k]);
-            if constexpr (COLS) gcol[w][k] = __builtin_fma(S[w], dxd[k], gcol[w][k]);
+            grow[k] = 0.0;
+            dxd[k] = (double)dxv[k];
           }
 #pragma unroll
-        for (int k = 0; k < DP; ++k)
-          if (k < d) atomicAdd(gacc + ci * DP + k, grow[k]);
+          for (int w = 0; w < WC; ++w)
+#pragma unroll
+            for (int k = 0; k < DP; ++k) {
+              grow[k] = __builtin_fma(S[w], dyd[w][k], grow[k]);
+              if constexpr (COLS) gcol[w][k] = __builtin_fma(S[w], dxd[k], gcol[w][k]);
+            }
+#pragma unroll
+          for (int k = 0; k < DP; ++k)
+            if (k < d) atomicAdd(gacc + ci * DP + k, grow[k]);
+        }
+        rcorner = right[0];
       }
-      rcorner = right[0];
+    }
+    if constexpr (COLS) {
+      if (!diag) {
+        // columns: H[j] = 4^-n sum over coarse column j; dK/dy_j = H[j-1] - H[j]
+        const double sy = inv_factor * (double)g;
+        float *gyb = p.gY + (long long)b * p.l2 * d;
+#pragma unroll
+        for (int w = 0; w < WC; ++w) {
+          const int jc = c0 / REP + lane * WC + w;
+          if (jc >= JC) continue;
+#pragma unroll
+          for (int k = 0; k < DP; ++k) {  // compile-time indices: a runtime bound would put gcol in scratch
+            if (k >= d) continue;
+            const float v = (float)(sy * gcol[w][k]);
+            unsafeAtomicAdd(gyb + (long long)(jc + 1) * d + k, v);
+            unsafeAtomicAdd(gyb + (long long)jc * d + k, -v);
+          }
+        }
+      }
     }
   }
   __syncthreads();  // the row accumulators are complete
   if (!ok) return;
 
   // dK/dx_i = G[i-1] - G[i] with G[r] = 4^-n gacc[r] (x2 for k(x, x)), times the upstream gradient
-  const float g = diag ? p.gout[a] : p.gout[(long long)a * p.n2 + b];
   const double sx = (diag ? 2.0 : 1.0) * inv_factor * (double)g;
   float *gxa = p.gX + (long long)a * p.l1 * d;
   for (int r = lane; r <= IC; r += 64)
@@ -330,22 +426,6 @@ __global__ __launch_bounds__(256) void pde_adj_kernel(PdeBwdArgs p) {
       const double gc = r < IC ? gacc[r * DP + k] : 0.0;
       unsafeAtomicAdd(gxa + (long long)r * d + k, (float)(sx * (gp - gc)));
     }
-  if (diag || !COLS) return;
-  // columns: H[j] = 4^-n sum over coarse column j; dK/dy_j = H[j-1] - H[j]
-  const double sy = inv_factor * (double)g;
-  float *gyb = p.gY + (long long)b * p.l2 * d;
-#pragma unroll
-  for (int w = 0; w < WC; ++w) {
-    const int jc = lane * WC + w;
-    if (jc >= JC) continue;
-#pragma unroll
-    for (int k = 0; k < DP; ++k) {  // compile-time indices: a runtime bound would put gcol in scratch
-      if (k >= d) continue;
-      const float v = (float)(sy * gcol[w][k]);
-      unsafeAtomicAdd(gyb + (long long)(jc + 1) * d + k, v);
-      unsafeAtomicAdd(gyb + (long long)jc * d + k, -v);
-    }
-  }
 }
 
 template <int DP, int W, int REP, int MODE>
@@ -353,13 +433,13 @@ static int launch_pde_adj(const PdeBwdArgs &a, long long nblocks, hipStream_t s)
   if constexpr (W < REP || REP * W > 64) {
     return GPSIG_EUNSUPPORTED;
   } else {
-    const size_t lds = (size_t)4 * (a.l1 - 1) * DP * 2 * sizeof(double);
+    const size_t lds = (size_t)a.wpb * pde_lds_wave_doubles(a.l1 - 1, DP) * sizeof(double);
     if (lds > 160 * 1024) return GPSIG_EUNSUPPORTED;
     // the column (dK/dy) accumulators only for cross pairs; k(x, x) takes twice the row part
     if (a.pair_mode == GPSIG_PAIRS_DIAG || MODE == 1)
-      hipLaunchKernelGGL((pde_adj_kernel<DP, W, REP, false, MODE>), dim3((unsigned)nblocks), dim3(256), lds, s, a);
+      hipLaunchKernelGGL((pde_adj_kernel<DP, W, REP, false, MODE>), dim3((unsigned)nblocks), dim3(64 * a.wpb), lds, s, a);
     else
-      hipLaunchKernelGGL((pde_adj_kernel<DP, W, REP, true, MODE>), dim3((unsigned)nblocks), dim3(256), lds, s, a);
+      hipLaunchKernelGGL((pde_adj_kernel<DP, W, REP, true, MODE>), dim3((unsigned)nblocks), dim3(64 * a.wpb), lds, s, a);
     return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
   }
 }

@@ -29,7 +29,7 @@ static int pde_adj_impl(int mode, const float *X, int n1, int l1, const float *Y
   if (row_end == row_begin) return GPSIG_OK;
   const int rows = row_end - row_begin;
   const int npairs = pair_mode == GPSIG_PAIRS_DIAG ? rows : rows * n2;
-  if (pde_front_floats(l1, l2, dyadic) == 0) return GPSIG_EUNSUPPORTED;  // J > 1024 or dyadic > 3
+  if (pde_front_floats(l1, l2, dyadic) == 0) return GPSIG_EUNSUPPORTED;  // dyadic > 3
   if (!workspace || workspace_bytes < gpsig_pde_vjp_workspace_bytes(npairs, l1, l2, dyadic)) return GPSIG_EWORKSPACE;
   PdeBwdArgs a{};
   a.X = X; a.Y = Y;
@@ -39,17 +39,22 @@ static int pde_adj_impl(int mode, const float *X, int n1, int l1, const float *Y
   a.gout = gout; a.gX = gX; a.gY = gY;
   a.fronts = static_cast<float *>(workspace);
   a.out = out;
+  // pairs per workgroup: 4 unless the per-wave LDS (row accumulators and dx of x) of long x needs fewer
+  const int dp = d <= 8 ? d : (d <= 16 ? 16 : 0);
+  int wpb = 4;
+  while (wpb > 1 && (size_t)wpb * pde_lds_wave_doubles(l1 - 1, dp) * sizeof(double) > 160 * 1024) wpb /= 2;
+  a.wpb = wpb;
   long long nblocks;
   if (pair_mode == GPSIG_PAIRS_DIAG) {
-    nblocks = (rows + 3) / 4;
+    nblocks = (rows + wpb - 1) / wpb;
   } else {
-    const int ta0 = row_begin / 4, ta1 = (row_end + 3) / 4;
+    const int ta0 = row_begin / wpb, ta1 = (row_end + wpb - 1) / wpb;
     a.ntb = n2;
     a.tiles_a0 = ta0;
     nblocks = (long long)(ta1 - ta0) * n2;
   }
   if (nblocks > 0x7fffffffLL) return GPSIG_EUNSUPPORTED;
-  switch (d <= 8 ? d : (d <= 16 ? 16 : 0)) {
+  switch (dp) {
 #define CASE(v) \
   case v: return pde_bwd_launch_dp<v>(a, nblocks, mode, s);
     CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) CASE(16)

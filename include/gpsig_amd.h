@@ -226,7 +226,8 @@ int gpsig_pde_diag(const float *X, int n, int l, int d, int dyadic, int solver, 
  * is re-solved on the mirrored wavefront and meets the forward sweep lane by lane; the workspace holds
  * the forward sweep's fronts (fp32, every few coarse steps, about (1 + REP/W) I J / H floats per pair;
  * I = 2^dyadic (l1-1), J = 2^dyadic (l2-1)), gpsig_pde_vjp_workspace_bytes(pairs, l1, l2, dyadic), which
- * returns 0 where the kernel does not apply (J > 1024 or dyadic > 3: GPSIG_EUNSUPPORTED). */
+ * returns 0 where the kernel does not apply (dyadic > 3: GPSIG_EUNSUPPORTED).  Wider grids than one
+ * wave's 64 W columns are swept in column blocks; their fp64 boundary columns are part of the workspace. */
 size_t gpsig_pde_vjp_workspace_bytes(int npairs, int l1, int l2, int dyadic);
 
 int gpsig_pde_vjp(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int dyadic, int solver,

@@ -88,7 +88,9 @@ def test_vjp_and_feature_entry_points_validate_arguments():
     # J = 18 fine columns at dyadic 1: W = 2 per lane, U = 9 lanes, 9 + 9 - 1 = 17 coarse steps, a front every
     # 32 / (2 * 2) = 8 steps -> 3 fronts of (W + REP) x 64 floats per pair
     assert lib.gpsig_pde_vjp_workspace_bytes(2, 10, 10, 1) == 2 * 3 * (2 + 2) * 64 * 4
-    assert lib.gpsig_pde_vjp_workspace_bytes(2, 10, 1100, 0) == 0  # J > 1024: unsupported
+    # J = 1099 > 64 x 16: two column blocks of 1024 (W = 16, H = 2, 36 fronts each) + fp64 boundary columns
+    assert lib.gpsig_pde_vjp_workspace_bytes(2, 10, 1100, 0) == 2 * (2 * 36 * 17 * 64 + 2 * 2 * 10) * 4
+    assert lib.gpsig_pde_vjp_workspace_bytes(2, 10, 10, 4) == 0  # dyadic > 3: unsupported
 
 
 def test_graph_capture_refuses_host_tensors_and_kernel_to():

@@ -149,3 +149,48 @@ def test_pde_fronts_forward_and_vjp(n, solver):
     Kg = kp.K(Xf)
     torch.testing.assert_close(Kg.detach(), kp.K(Xf.detach()), rtol=1e-7, atol=0)
     assert torch.equal(Kg, Kg.T)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("L,n,d", [(600, 1, 3), (150, 3, 3), (1100, 0, 5)])
+def test_pde_kdiag_vjp_column_blocks(L, n, d):
+    """Grids wider than one wave's 64 W refined columns, swept in column blocks: 1198 columns = 2 blocks of
+    1024 (W = 16), 1192 at dyadic order 3 = 3 blocks of 512 (W = 8), and 1099 at order 0 with d = 5, where
+    x's per-pair LDS (row accumulators and increments, 66 KB) leaves 2 pairs per workgroup."""
+    from gpsig_amd import ops
+    rng = np.random.default_rng(L + n)
+    X = np.cumsum(rng.standard_normal((3, L, d)), 1) / np.sqrt(L * d) * 2
+    w = rng.standard_normal(3)
+    K, Kr = pde.pde_diag_grids(X, n, 1)
+    ref = pde_grad.kdiag_grad(X, np.tril(K), np.tril(Kr), n) * w[:, None, None]
+    got = ops.pde_diag_vjp(torch.tensor(X, device=DEV), torch.tensor(w, device=DEV), n, 1)
+    assert norm_rel_err(got.cpu().numpy(), ref) < 1e-5
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("l2,n,solver", [(1500, 0, 1), (300, 2, 1), (1500, 0, 0)])
+def test_pde_cross_vjp_column_blocks(l2, n, solver):
+    """Cross pairs in column blocks (J = 1499 at order 0, 1196 at order 2: 2 blocks of 1024), against the
+    adjoint restated from the reference; then the training-step split (gpsig_pde_fronts forward, whose
+    values equal gpsig_pde_gram's, and gpsig_pde_vjp_fronts) against the one-launch adjoint."""
+    from gpsig_amd import ops
+    rng = np.random.default_rng(l2 + n)
+    X = np.cumsum(rng.standard_normal((3, 12, 2)), 1) * 0.3
+    Y = np.cumsum(rng.standard_normal((2, l2, 2)), 1) * 0.3 / np.sqrt(l2 / 10)
+    G = rng.standard_normal((3, 2))
+    Xt, Yt, Gt = (torch.tensor(v, device=DEV, dtype=torch.float32) for v in (X, Y, G))
+    gX, gY = ops.pde_gram_vjp(Xt, Yt, Gt, n, solver)
+    rx, ry = np.zeros_like(X), np.zeros_like(Y)
+    for a in range(3):
+        for b in range(2):
+            gx, gy = pde_grad.pair_grad(X[a], Y[b], n, solver)
+            rx[a] += G[a, b] * gx
+            ry[b] += G[a, b] * gy
+    assert norm_rel_err(gX.cpu().numpy(), rx) < 1e-5
+    assert norm_rel_err(gY.cpu().numpy(), ry) < 1e-5
+    fr = torch.empty(ops.pde_fronts_bytes(6, 12, l2, n) // 4, device=DEV)
+    K = ops.pde_fronts(Xt, Yt, n, solver, fr)
+    torch.testing.assert_close(K, ops.pde_gram(Xt, Yt, n, solver), rtol=0, atol=0)
+    fX, fY = ops.pde_vjp_fronts(Xt, Yt, Gt, n, solver, fr)
+    assert norm_rel_err(fX.cpu().numpy(), gX.cpu().numpy()) < 1e-6
+    assert norm_rel_err(fY.cpu().numpy(), gY.cpu().numpy()) < 1e-6
