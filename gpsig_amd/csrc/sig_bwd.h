@@ -746,33 +746,49 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
 #pragma unroll
           for (int c = 0; c < DP; ++c) dxv[c] = fr[DP + c];
           const float g = fr[2 * DP + 1];
-          float dM[W], kn[W], Eqn[W], mx[W];
+          float dM[W], kn[W], Eqn[W], mx[W], pp[W], cv[W];
           bool slow = false;
+          // p along the lane's columns by p_{j+1} = p_j + c_j and Ep_{j+1} = Ep_j + (1 + Ep_j) Ec_j from
+          // the exact first column (the forward seed's column recurrence, RbfSeedPk::row: the chain
+          // anchors fall on the same columns, multiples of 4)
 #pragma unroll
           for (int w = 0; w < W; ++w) {
-            float pp = -g, c = 0.0f;
+            float c = dy[w][0] * dxv[0];
 #pragma unroll
-            for (int k = 0; k < DP; ++k) {
-              pp = __builtin_fmaf(y[w][k], dxv[k], pp);
-              c = __builtin_fmaf(dy[w][k], dxv[k], c);
-            }
-            const float Ep = em1_small(pp), Ec = em1_small(c);
+            for (int k = 1; k < DP; ++k) c = __builtin_fmaf(dy[w][k], dxv[k], c);
+            cv[w] = c;
+          }
+          pp[0] = -g;
+#pragma unroll
+          for (int k = 0; k < DP; ++k) pp[0] = __builtin_fmaf(y[0][k], dxv[k], pp[0]);
+#pragma unroll
+          for (int w = 1; w < W; ++w) pp[w] = pp[w - 1] + cv[w - 1];
+          float Ep = em1_small(pp[0]);
+#pragma unroll
+          for (int w = 0; w < W; ++w) {
+            const float c = cv[w], Ec = em1_small(c);
             float t = __builtin_fmaf(Ep, Ec, Ec);
+            const float Epw = Ep;
+            Ep += t;
             t = __builtin_fmaf(Eq[w], t, t);
-            dM[w] = kc[w] * __builtin_fmaf(Ep, Eq[w], t);
-            kn[w] = __builtin_fmaf(kc[w], Ep, kc[w]);
+            dM[w] = kc[w] * __builtin_fmaf(Epw, Eq[w], t);
+            kn[w] = __builtin_fmaf(kc[w], Epw, kc[w]);
             Eqn[w] = __builtin_fmaf(Eq[w], Ec, Eq[w] + Ec);
-            mx[w] = __builtin_fmaxf(__builtin_fabsf(pp), __builtin_fabsf(c));
+            mx[w] = __builtin_fmaxf(__builtin_fabsf(pp[w]), __builtin_fabsf(c));
             slow = slow || !(mx[w] < EM1_TAU);
           }
           if (__builtin_amdgcn_ballot_w64(slow) != 0) {
+            // out-of-range cells may have spoilt the chained Ep: in-range cells from their own p
             exact_row(fr + FS, kn, Eqn);
             const float knR = lane_next(kn[0]), kcR2 = lane_next(kc[0]);
 #pragma unroll
             for (int w = 0; w < W; ++w) {
               const float kn1 = (w + 1 < W) ? kn[w + 1] : knR;
               const float kc1 = (w + 1 < W) ? kc[w + 1] : kcR2;
-              if (!(mx[w] < EM1_TAU)) dM[w] = (kn1 - kn[w]) - (kc1 - kc[w]);
+              const float Epd = em1_small(pp[w]), Ecd = em1_small(cv[w]);
+              float t = __builtin_fmaf(Epd, Ecd, Ecd);
+              t = __builtin_fmaf(Eq[w], t, t);
+              dM[w] = (mx[w] < EM1_TAU) ? kc[w] * __builtin_fmaf(Epd, Eq[w], t) : (kn1 - kn[w]) - (kc1 - kc[w]);
             }
           }
 #pragma unroll

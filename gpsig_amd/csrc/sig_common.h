@@ -245,6 +245,7 @@ struct RbfSeedPk {
   f2 Eq[W2], kc[W2];  // expm1(q_ij), k(x_i, y_j)
   float kcR;          // next lane's kc of its first column
   bool valid_last;
+  bool clo = false;   // every |c_ij| of the wave < EM1_LO_TAU: Ec by the cubic (bound_c)
 
   GPSIG_DEV void init(const float *__restrict__ fx, const float *__restrict__ fy, int gl, int l2) {
     const int ncols = l2 - 1;
@@ -274,6 +275,19 @@ struct RbfSeedPk {
     for (int k = 0; k < DP; ++k) x0[k] = fx[k];
     exact(x0, Eq, kc);
     kcR = lane_next(kc[0][0]);
+  }
+
+  // |c_ij| = |<dx_i, dy_j>| <= 2 sqrt(hdx_i hdy_j) (Cauchy-Schwarz on the records' |d|^2/2): when the
+  // bound over all rows of x and all columns of the wave stays below EM1_LO_TAU (with margin for the
+  // records' rounding), every Ec of the pair block takes the cubic (wave-uniform, once per block).
+  GPSIG_DEV void bound_c(const float *__restrict__ fx, int nrows) {
+    float hx = 0.0f, hy = 0.0f;
+    for (int i = (int)__lane_id(); i < nrows; i += 64) hx = __builtin_fmaxf(hx, fx[(long long)i * FS + 2 * DP]);
+#pragma unroll
+    for (int w2 = 0; w2 < W2; ++w2) hy = __builtin_fmaxf(hy, __builtin_fmaxf(hdy[w2][0], hdy[w2][1]));
+    hx = wave_max(hx);
+    hy = wave_max(hy);
+    clo = wave_uniform(4.0f * hx * hy < 0.98f * EM1_LO_TAU * EM1_LO_TAU ? 1 : 0) != 0;
   }
 
   // expm1(q) and k(x, y) of the row with point x, evaluated from x - y
@@ -320,20 +334,111 @@ struct RbfSeedPk {
 
   // Cells of row i into dM.  anch (wave-uniform): the next row's state is re-evaluated exactly
   // instead of by the recurrences.
+  //
+  // Column recurrence of the p side: p_{i,j+1} - p_ij = <y_{j+1} - y_j, dx_i> = c_ij, so
+  //   p_{i,j+1} = p_ij + c_ij,   Ep_{i,j+1} = expm1(p_ij + c_ij) = Ep_ij + (1 + Ep_ij) Ec_ij
+  // and (1 + Ep) Ec is a term the cell needs anyway.  Only column pair 0 (the lane's columns 0 and
+  // W/2) takes the dot and the polynomial; pairs 1 .. W/2-1 follow in-lane (two operations each instead
+  // of D + 6).  Rows with a cell outside the polynomial range re-evaluate every Ep directly (slow path).
+#ifndef GPSIG_PCHAIN
+#define GPSIG_PCHAIN 1
+#endif
+  // CLO: the pair block's |c| bound holds (bound_c): Ec by the cubic, and only |p| is range-checked.
+  template <bool CLO = false>
   GPSIG_DEV void row(const Row &rd, bool anch, f2 (&dM)[W2]) {
     f2 p[W2], c[W2];
+    if constexpr (!GPSIG_PCHAIN) {  // A/B arm: every pair's dots and polynomials evaluated directly
+#pragma unroll
+      for (int w2 = 0; w2 < W2; ++w2) {
+        f2 a = splat2(-rd.g), cc = splat2(0.0f);
+#pragma unroll
+        for (int k = 0; k < DP; ++k) {
+          a = fma2(y[w2][k], splat2(rd.dx[k]), a);
+          cc = fma2(dy[w2][k], splat2(rd.dx[k]), cc);
+        }
+        p[w2] = a;
+        c[w2] = cc;
+      }
+      row_pc(rd, anch, p, c, dM);
+      return;
+    }
 #pragma unroll
     for (int w2 = 0; w2 < W2; ++w2) {
-      f2 a = splat2(-rd.g), cc = splat2(0.0f);
+      f2 cc = dy[w2][0] * splat2(rd.dx[0]);
 #pragma unroll
-      for (int k = 0; k < DP; ++k) {
-        a = fma2(y[w2][k], splat2(rd.dx[k]), a);
-        cc = fma2(dy[w2][k], splat2(rd.dx[k]), cc);
-      }
-      p[w2] = a;
+      for (int k = 1; k < DP; ++k) cc = fma2(dy[w2][k], splat2(rd.dx[k]), cc);
       c[w2] = cc;
     }
-    row_pc(rd, anch, p, c, dM);
+    {
+      f2 a = splat2(-rd.g);
+#pragma unroll
+      for (int k = 0; k < DP; ++k) a = fma2(y[0][k], splat2(rd.dx[k]), a);
+      p[0] = a;
+    }
+#pragma unroll
+    for (int w2 = 1; w2 < W2; ++w2) p[w2] = p[w2 - 1] + c[w2 - 1];
+    f2 Ec[W2], Ep[W2];
+    if constexpr (CLO)
+      em1_lo2_n<W2>(c, Ec);
+    else
+      em1_small2_n<W2>(c, Ec);
+    Ep[0] = em1_small2(p[0]);
+    float mx = 0.0f;
+#pragma unroll
+    for (int w2 = 0; w2 < W2; ++w2) {
+      const f2 t = fma2(Ep[w2], Ec[w2], Ec[w2]);  // (1 + Ep) Ec
+      if (w2 + 1 < W2) Ep[w2 + 1] = Ep[w2] + t;
+      const f2 t2 = fma2(Eq[w2], t, t);
+      dM[w2] = kc[w2] * fma2(Ep[w2], Eq[w2], t2);
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        if constexpr (CLO)  // |c| < EM1_LO_TAU < EM1_TAU a priori
+          mx = __builtin_fmaxf(mx, __builtin_fabsf(p[w2][h]));
+        else
+          mx = __builtin_fmaxf(__builtin_fmaxf(mx, __builtin_fabsf(p[w2][h])), __builtin_fabsf(c[w2][h]));
+      }
+    }
+    const bool slow = GPSIG_NAIVE && __builtin_amdgcn_ballot_w64(mx >= EM1_TAU) != 0;
+    if (anch || slow) {
+      f2 Eqn[W2], kn[W2];
+      next_exact(rd, Eqn, kn);
+      const float knR = lane_next(kn[0][0]);
+      if (slow) {
+        // a cell outside the polynomial range may have spoilt the chained Ep of the pairs after it:
+        // every in-range cell is re-evaluated from its own p, the others take the corner difference
+        f2 Epd[W2], Ecd[W2];
+        em1_small2_n<W2>(p, Epd);
+        em1_small2_n<W2>(c, Ecd);
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          const int w2 = w % W2, h = w / W2;
+          const float kn1 = (w + 1 < W) ? kn[(w + 1) % W2][(w + 1) / W2] : knR;
+          const float kc1 = (w + 1 < W) ? kc[(w + 1) % W2][(w + 1) / W2] : kcR;
+          const float naive = (kn1 - kn[w2][h]) - (kc1 - kc[w2][h]);
+          const float m = __builtin_fmaxf(__builtin_fabsf(p[w2][h]), __builtin_fabsf(c[w2][h]));
+          float t = __builtin_fmaf(Epd[w2][h], Ecd[w2][h], Ecd[w2][h]);
+          t = __builtin_fmaf(Eq[w2][h], t, t);
+          const float prod = kc[w2][h] * __builtin_fmaf(Epd[w2][h], Eq[w2][h], t);
+          float v = m < EM1_TAU ? prod : naive;
+          if (w + 1 == W && !valid_last) v = 0.0f;
+          dM[w2][h] = v;
+        }
+      }
+#pragma unroll
+      for (int w2 = 0; w2 < W2; ++w2) {
+        Eq[w2] = Eqn[w2];
+        kc[w2] = kn[w2];
+      }
+      kcR = knR;
+    } else {
+      // row-to-row recurrences in place (the cells above were the last readers of kc and Eq)
+#pragma unroll
+      for (int w2 = 0; w2 < W2; ++w2) {
+        kc[w2] = fma2(kc[w2], Ep[w2], kc[w2]);
+        Eq[w2] = fma2(Eq[w2], Ec[w2], Eq[w2] + Ec[w2]);
+      }
+      kcR = lane_next(kc[0][0]);
+    }
   }
 
   // The increment inner products of 4 consecutive rows i0 .. i0+3 on the matrix cores

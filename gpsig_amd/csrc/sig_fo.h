@@ -102,6 +102,10 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
     const int npts = nblk == 1 ? p.l2 : min(p.l2 - j0, Seed::DIFF ? CPB + 1 : CPB);
     PSeed seed;
     seed.init(fx, fy + (long long)j0 * FS, gl, npts);
+#ifndef GPSIG_CLO
+#define GPSIG_CLO 1
+#endif
+    if constexpr (PK && !MF && SPLIT != 2 && GPSIG_CLO) seed.bound_c(fx, nrows);
 
     f2 C[M][W2];
 #pragma unroll
@@ -112,7 +116,7 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
     // One row: seed cells, then the level recursion.  S_m = exclusive prefix over (rows < i, cols < j)
     // of R_m = exclusive scan over j of C_m; the M-1 scans are independent and interleave.
     using Rec = std::conditional_t<PK, typename RbfSeedPk<DP, W>::Row, RowData<DP>>;
-    auto do_row = [&](int i, const Rec &rd, bool anch, const f2 *pc = nullptr) {
+    auto do_row = [&](auto clo_t, int i, const Rec &rd, bool anch, const f2 *pc = nullptr) {
       f2 dM[W2];
       if constexpr (SPLIT == 2) {
         const f4 *src = reinterpret_cast<const f4 *>(dms + (long long)i * (LP * W));
@@ -132,7 +136,7 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
           }
           seed.row_pc(rd, anch, pp, cc, dM);
         } else {
-          seed.row(rd, anch, dM);
+          seed.template row<decltype(clo_t)::value>(rd, anch, dM);
         }
       } else {
         float d1[W];
@@ -208,31 +212,42 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
             pc[w2] = (f2){P[w2][r], P[w2 + W2][r]};
             pc[W2 + w2] = (f2){Q[w2][r], Q[w2 + W2][r]};
           }
-          do_row(i + r, rd, r == 3 && ((i + 3) % PSeed::ANCHOR) == PSeed::ANCHOR - 1, pc);
+          do_row(std::false_type{}, i + r, rd, r == 3 && ((i + 3) % PSeed::ANCHOR) == PSeed::ANCHOR - 1, pc);
         }
       }
     }
-    if constexpr (PK && GPSIG_FO_UNROLL2 && !MF) {
-      // row pairs: ANCHOR is even, so the first row of a pair never anchors (compile-time)
-      static_assert(PSeed::ANCHOR % 2 == 0, "anchor period");
-      for (; i + 2 <= nrows; i += 2) {
-        Rec r0, r1;
-        r0.load(fx, i);
-        r1.load(fx, i + 1);
-        do_row(i, r0, false);
-        do_row(i + 1, r1, ((i + 1) % PSeed::ANCHOR) == PSeed::ANCHOR - 1);
+    // the rest of the rows, in a copy per Ec polynomial (the pair block's |c| bound, bound_c)
+    auto run_rows = [&](auto clo_t) {
+      if constexpr (PK && GPSIG_FO_UNROLL2 && !MF) {
+        // row pairs: ANCHOR is even, so the first row of a pair never anchors (compile-time)
+        static_assert(PSeed::ANCHOR % 2 == 0, "anchor period");
+        for (; i + 2 <= nrows; i += 2) {
+          Rec r0, r1;
+          r0.load(fx, i);
+          r1.load(fx, i + 1);
+          do_row(clo_t, i, r0, false);
+          do_row(clo_t, i + 1, r1, ((i + 1) % PSeed::ANCHOR) == PSeed::ANCHOR - 1);
+        }
       }
-    }
-    for (; i < nrows; ++i) {
-      Rec rd;
-      bool anch = true;
-      if constexpr (PK) {
-        rd.load(fx, i);
-        anch = (i % PSeed::ANCHOR) == PSeed::ANCHOR - 1;
-      } else {
-        rd.load(fx, i, SEED);
+      for (; i < nrows; ++i) {
+        Rec rd;
+        bool anch = true;
+        if constexpr (PK) {
+          rd.load(fx, i);
+          anch = (i % PSeed::ANCHOR) == PSeed::ANCHOR - 1;
+        } else {
+          rd.load(fx, i, SEED);
+        }
+        do_row(clo_t, i, rd, anch);
       }
-      do_row(i, rd, anch);
+    };
+    if constexpr (PK && !MF && SPLIT != 2) {
+      if (seed.clo)
+        run_rows(std::true_type{});
+      else
+        run_rows(std::false_type{});
+    } else {
+      run_rows(std::false_type{});
     }
 
     // ---- saved VJP state (gpsig_sig_gram_state): column sums of levels 1..M-1 (column pair k holds
