@@ -23,7 +23,9 @@ here = os.path.dirname(os.path.abspath(__file__))
 
 def is_gram(name):
     # sig_fo_kernel<DP, W, LP, M, SEED, DIAGK = false, SAVE = false, MF = false>
-    return "sig_fo_kernel" in name and ("false, false, false>" in name or "Lb0ELb0ELb0E" in name)
+    # (a 9th argument, SPLIT = 0, follows MF in builds with the split diagnostic)
+    return "sig_fo_kernel" in name and ("false, false, false>" in name or "false, false, false, 0>" in name
+                                        or "Lb0ELb0ELb0E" in name)
 
 
 def one(pattern):
