@@ -159,14 +159,21 @@ __global__ __launch_bounds__(256) void pde_kernel(PdeArgs p) {
 // the next block through this wave's LDS slab `bnd` (I + 1 doubles), where lane 0 reads it as its left
 // boundary; lane 0 reads row i at step i and the last lane overwrites it at step i + 63, so one slab
 // serves every block in place.
-template <typename T, int DP, int W, int REP, int SOLVER>
+//
+// LP < 64 (Gram pairs, grids of at most LP W fine columns): G = 64 / LP pairs (a, b..b+G-1) per wave, one
+// lane group of LP lanes each, sharing x's increments.  Fewer lanes per pair shorten the skew (IC + U - 1
+// steps for U lanes) and leave fewer lanes idle, at W columns per lane.
+template <typename T, int DP, int W, int REP, int SOLVER, int LP = 64>
 __global__ __launch_bounds__(256) void pde_rep_kernel(PdeArgs p) {
   static_assert(W % REP == 0, "a lane owns whole coarse columns");
+  static_assert(LP == 16 || LP == 32 || LP == 64, "lane group");
   constexpr int WC = W / REP;
-  constexpr int CB = 64 * W;  // fine columns per block
+  constexpr int G = 64 / LP;
+  constexpr int CB = LP * W;  // fine columns per block (G > 1: one block)
   extern __shared__ __attribute__((aligned(16))) float lds[];
   const int lane = threadIdx.x & 63;
   const int wave = wave_uniform(threadIdx.x >> 6);
+  const int g = lane / LP, gl = lane % LP;
 
   int a, b;
   if (p.pair_mode == GPSIG_PAIRS_DIAG) {
@@ -175,7 +182,7 @@ __global__ __launch_bounds__(256) void pde_rep_kernel(PdeArgs p) {
   } else {
     int ta, tb;
     if (p.pair_mode == GPSIG_PAIRS_UPPER) {
-      const Tile t = upper_tile(p.tile_base + (long long)blockIdx.x, p.ntb, 4);
+      const Tile t = upper_tile(p.tile_base + (long long)blockIdx.x, p.ntb, 4 / G);
       ta = t.ta;
       tb = t.tb;
     } else {
@@ -183,12 +190,15 @@ __global__ __launch_bounds__(256) void pde_rep_kernel(PdeArgs p) {
       tb = (int)blockIdx.x % p.ntb;
     }
     a = ta * 4 + wave;
-    b = tb;
+    b = tb * G + g;
   }
-  // wave-uniform validity; every wave still reaches the LDS barrier below
-  bool ok = a >= p.row_begin && a < p.row_end && b < p.n2;
-  if (p.pair_mode == GPSIG_PAIRS_UPPER && b < a) ok = false;
-  if (!ok) { a = p.row_begin; b = p.pair_mode == GPSIG_PAIRS_RECT ? 0 : a; }
+  // a is wave-uniform; b per lane group (G > 1: an invalid group computes on a clamped pair, stores nothing)
+  const bool aok = a >= p.row_begin && a < p.row_end;
+  bool bok = b < p.n2;
+  if (p.pair_mode == GPSIG_PAIRS_UPPER && b < a) bok = false;
+  const bool ok = aok && bok;  // wave-uniform when G == 1
+  if (!aok) a = p.row_begin;
+  if (!bok) b = p.pair_mode == GPSIG_PAIRS_RECT ? 0 : a;
 
   const T inv_factor = (T)1.0 / (T)(REP * REP);
   const int IC = p.l1 - 1, JC = p.l2 - 1;  // coarse rows / columns
@@ -204,22 +214,25 @@ __global__ __launch_bounds__(256) void pde_rep_kernel(PdeArgs p) {
     for (int k = 0; k < DP; ++k) dxs[r * DP + k] = k < d ? x[(r + 1) * d + k] - x[r * d + k] : 0.0f;
   T *bnd = reinterpret_cast<T *>(lds + (((size_t)4 * IC * DP + 3) & ~(size_t)3)) + (size_t)wave * (I + 1);
   __syncthreads();
-  if (!ok) return;
+  if (!aok || (G == 1 && !ok)) return;
 
   const bool hybrid = (p.pair_mode == GPSIG_PAIRS_DIAG) && SOLVER == 0;
   constexpr bool s1 = SOLVER == 1;
+  // coarse increments of a lane's columns as packed fp32 pairs (2w, 2w + 1): the dots of a step are
+  // v_pk_fma_f32 with x's increment broadcast
+  constexpr int WC2 = (WC + 1) / 2;
   T up[W];
   for (int blk = 0; blk < nblk; ++blk) {
     const int c0 = blk * CB;  // first fine column of the block (a multiple of REP)
     const bool from_left = blk > 0, to_right = blk + 1 < nblk;
     // y increments of this lane's coarse columns
-    float dy[WC][DP];
+    f2 dy[WC2][DP];
 #pragma unroll
-    for (int w = 0; w < WC; ++w) {
-      int cj = c0 / REP + lane * WC + w;
+    for (int w = 0; w < 2 * WC2; ++w) {
+      int cj = c0 / REP + gl * WC + w;
       cj = cj < JC - 1 ? cj : JC - 1;
 #pragma unroll
-      for (int k = 0; k < DP; ++k) dy[w][k] = k < d ? y[(cj + 1) * d + k] - y[cj * d + k] : 0.0f;
+      for (int k = 0; k < DP; ++k) dy[w / 2][k][w % 2] = (k < d && w < WC) ? y[(cj + 1) * d + k] - y[cj * d + k] : 0.0f;
     }
 #pragma unroll
     for (int w = 0; w < W; ++w) up[w] = (T)1;
@@ -227,28 +240,34 @@ __global__ __launch_bounds__(256) void pde_rep_kernel(PdeArgs p) {
 #pragma unroll
     for (int r = 0; r < REP; ++r) last[r] = (T)1;
     T corner_prev = (T)1;  // left boundary of the previous step's last row
-    const int lanes_used = min(64, (J - c0 + W - 1) / W);
+    const int lanes_used = min(LP, (J - c0 + W - 1) / W);
     const int nsteps = IC + lanes_used - 1;
     for (int s = 0; s < nsteps; ++s) {
       T left[REP];
 #pragma unroll
       for (int r = 0; r < REP; ++r) {
         left[r] = lane_prev(last[r]);
-        if (lane == 0) left[r] = from_left ? bnd[min(s * REP + r + 1, I)] : (T)1;
+        if (gl == 0) left[r] = (G == 1 && from_left) ? bnd[min(s * REP + r + 1, I)] : (T)1;
       }
-      const int ci = s - lane;
-      if (ci >= 0 && ci < IC && lane < lanes_used) {
+      const int ci = s - gl;
+      if (ci >= 0 && ci < IC && gl < lanes_used) {
         const float *dxr = dxs + ci * DP;
         float dxv[DP];
 #pragma unroll
         for (int k = 0; k < DP; ++k) dxv[k] = dxr[k];
+        f2 incp[WC2];
+#pragma unroll
+        for (int w2 = 0; w2 < WC2; ++w2) {
+          f2 acc = dy[w2][0] * splat2(dxv[0]);
+#pragma unroll
+          for (int k = 1; k < DP; ++k) acc = fma2(dy[w2][k], splat2(dxv[k]), acc);
+          incp[w2] = acc;
+        }
         // coefficients of the lane's coarse cells: solver 1 uses (A, B), solver 0 uses inc - 1 (as B)
         T A[WC], B[WC];
 #pragma unroll
         for (int w = 0; w < WC; ++w) {
-          float incf = 0.0f;
-#pragma unroll
-          for (int k = 0; k < DP; ++k) incf = __builtin_fmaf(dxv[k], dy[w][k], incf);
+          const float incf = incp[w / 2][w % 2];
           const T inc = (T)incf * inv_factor;
           const T inc2 = inc * inc;
           if constexpr (s1) {
@@ -286,7 +305,7 @@ __global__ __launch_bounds__(256) void pde_rep_kernel(PdeArgs p) {
           }
           last[r] = lft;
         }
-        if (to_right && lane == 63) {
+        if (G == 1 && to_right && lane == 63) {
 #pragma unroll
           for (int r = 0; r < REP; ++r) bnd[ci * REP + r + 1] = last[r];
         }
@@ -300,7 +319,7 @@ __global__ __launch_bounds__(256) void pde_rep_kernel(PdeArgs p) {
 #pragma unroll
   for (int w = 0; w < W; ++w)
     if (w == slot) res = up[w];
-  if (lane == owner) {
+  if (gl == owner && ok) {
     const float v = (float)res;
     if (p.pair_mode == GPSIG_PAIRS_DIAG) {
       p.out[a] = v;
@@ -337,6 +356,58 @@ static int launch_pde_rep(const PdeArgs &a, long long nblocks, hipStream_t s) {
   }
 }
 
+// Lane-group geometry for Gram pairs (solver 1, the reference's default): G = 64 / LP pairs per wave,
+// W fine columns per lane with LP W >= J (no column blocks).  Per pair the wave issues about
+// steps (3 REP W + (DP/2 + 7) W/REP + 2 REP + 12) / G instructions, steps = IC + ceil(J/W) - 1
+// (the skew); the smallest estimate among LP = 16, 32 (W = 8, 16, 24) and the one-pair-per-wave
+// geometry of pde_rep_w wins.  GPSIG_PDE_LP = 16 / 32 / 64 pins the lane group (A/B).
+struct PdeLp { int LP, W; };
+inline double pde_cost(int IC, int J, int REP, int DP, int W, int G) {
+  const int U = (J + W - 1) / W;
+  return (double)(IC + U - 1) * (3.0 * REP * W + (DP / 2.0 + 7.0) * W / REP + 2.0 * REP + 12.0) / G;
+}
+inline int pde_w64(int J, int REP) {  // W of pde_rep_w's one-pair-per-wave geometry
+  if (J <= 64 * REP) return REP;
+  if (J <= 128 * REP && 2 * REP <= 16) return 2 * REP;
+  if (REP <= 4 && J <= 192 * REP) return 3 * REP;
+  return 4 * REP;
+}
+inline PdeLp pde_pick_lp(int IC, int J, int REP, int DP) {
+  static const int force = [] { const char *e = getenv("GPSIG_PDE_LP"); return e ? atoi(e) : 0; }();
+  PdeLp best{64, 0};
+  if (force == 64) return best;
+  double bc = pde_cost(IC, J, REP, DP, pde_w64(J, REP), 1);
+  for (int LP : {16, 32})
+    for (int W : {8, 16, 24}) {
+      if (W % REP || LP * W < J || (W / REP) * DP > 64) continue;
+      if (force && force != LP) continue;
+      const double c = pde_cost(IC, J, REP, DP, W, 64 / LP);
+      if (force ? (best.LP == 64 || c < bc) : c < bc) { bc = c; best = {LP, W}; }
+    }
+  return best;
+}
+
+template <typename T, int DP, int W, int REP, int LP>
+static int launch_pde_lp(const PdeArgs &a, long long nblocks, hipStream_t s) {
+  if constexpr (W % REP != 0 || (W / REP) * DP > 64) {
+    return GPSIG_EUNSUPPORTED;
+  } else {
+    const size_t lds = ((size_t)4 * (a.l1 - 1) * DP + 3) / 4 * 4 * sizeof(float);
+    if (lds > 160 * 1024) return GPSIG_EUNSUPPORTED;
+    hipLaunchKernelGGL((pde_rep_kernel<T, DP, W, REP, 1, LP>), dim3((unsigned)nblocks), dim3(256), lds, s, a);
+    return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
+  }
+}
+
+template <typename T, int DP, int REP>
+static int pde_lp_dispatch(const PdeArgs &a, long long nblocks, PdeLp g, hipStream_t s) {
+#define GPSIG_LPW(lp, w) \
+  if (g.LP == lp && g.W == w) return launch_pde_lp<T, DP, w, REP, lp>(a, nblocks, s);
+  GPSIG_LPW(16, 8) GPSIG_LPW(16, 16) GPSIG_LPW(16, 24) GPSIG_LPW(32, 8) GPSIG_LPW(32, 16) GPSIG_LPW(32, 24)
+#undef GPSIG_LPW
+  return GPSIG_EUNSUPPORTED;
+}
+
 // W = the smallest multiple of REP with J / W <= 64 lanes (-1: use the per-row kernel)
 template <typename T, int DP, int REP>
 static int pde_rep_w(const PdeArgs &a, long long nblocks, int J, hipStream_t s) {
@@ -362,7 +433,13 @@ static int launch_pde(const PdeArgs &a, long long nblocks, hipStream_t s) {
 }
 
 template <typename T, int DP>
-static int pde_w(const PdeArgs &a, long long nblocks, int J, hipStream_t s) {
+static int pde_w(const PdeArgs &a, long long nblocks, int J, PdeLp g, hipStream_t s) {
+  if (g.LP != 64) {
+    if (a.dyadic == 0) return pde_lp_dispatch<T, DP, 1>(a, nblocks, g, s);
+    if (a.dyadic == 1) return pde_lp_dispatch<T, DP, 2>(a, nblocks, g, s);
+    if (a.dyadic == 2) return pde_lp_dispatch<T, DP, 4>(a, nblocks, g, s);
+    return GPSIG_EUNSUPPORTED;
+  }
   {
     int rc = -1;
     if (a.dyadic == 0) rc = pde_rep_w<T, DP, 1>(a, nblocks, J, s);
@@ -387,27 +464,35 @@ int pde_launch(const float *X, int n1, int l1, const float *Y, int n2, int l2, i
   a.dyadic = dyadic; a.solver = solver;
   a.pair_mode = pair_mode; a.row_begin = row_begin; a.row_end = row_end;
   a.out = out; a.out_row0 = out_row0; a.out_rows = out_rows; a.out_ld = out_ld;
+  const int J = (1 << dyadic) * (l2 - 1);
+  const int DPI = d <= 8 ? d : 16;
+  // lane groups of Gram pairs: solver 1, dyadic <= 2, d <= 8 (pde_pick_lp)
+  PdeLp lpg{64, 0};
+  if (pair_mode != GPSIG_PAIRS_DIAG && solver == 1 && dyadic <= 2 && d <= 8 && l1 >= 2 && l2 >= 2)
+    lpg = pde_pick_lp(l1 - 1, J, 1 << dyadic, DPI);
+  const int G = 64 / lpg.LP;
   long long nblocks;
   if (pair_mode == GPSIG_PAIRS_DIAG) {
     nblocks = (row_end - row_begin + 3) / 4;
   } else {
     const int ta0 = row_begin / 4, ta1 = (row_end + 3) / 4;
-    a.ntb = n2;
+    const int ntb = (n2 + G - 1) / G;
+    a.ntb = ntb;
     a.tiles_a0 = ta0;
     if (pair_mode == GPSIG_PAIRS_RECT) {
-      nblocks = (long long)(ta1 - ta0) * n2;
+      nblocks = (long long)(ta1 - ta0) * ntb;
     } else {
-      auto P = [&](long long r) { return r * (long long)n2 - 4LL * r * (r - 1) / 2; };
+      const long long k = 4 / G;
+      auto P = [&](long long r) { return r * (long long)ntb - k * r * (r - 1) / 2; };
       a.tile_base = P(ta0);
       nblocks = P(ta1) - a.tile_base;
     }
   }
   if (nblocks <= 0) return GPSIG_OK;
-  const int J = (1 << dyadic) * (l2 - 1);
   using T = double;  // fp64 solution grid (the reference's float64), fp32 increments (as the CUDA op, .cu:27)
   switch (d <= 8 ? d : (d <= 16 ? 16 : 0)) {
 #define CASE(v) \
-  case v: return pde_w<T, v>(a, nblocks, J, s);
+  case v: return pde_w<T, v>(a, nblocks, J, lpg, s);
     CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) CASE(16)
 #undef CASE
     default: return GPSIG_EUNSUPPORTED;
