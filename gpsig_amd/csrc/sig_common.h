@@ -241,14 +241,40 @@ struct RbfSeedPk {
   static constexpr int ANCHOR = GPSIG_PK_ANCHOR;
   static constexpr float NHL2E = -0.72134752044448170f;  // exp(-d2/2) = exp2(d2 * NHL2E)
   static constexpr float L2E = 1.4426950408889634f;
-  f2 y[W2][DP], dy[W2][DP], hdy[W2];
+  // Wide channels (DP >= GPSIG_YG_DP): only column pair 0's points stay in registers (the rows' p dots
+  // need them, the other pairs' p follow by the column recurrence); the others are needed only on
+  // anchor and slow rows (exact) and are re-read from the records there.  This keeps W = 8 columns per
+  // lane within 256 VGPRs at D = 6..8.
+#ifndef GPSIG_YG_DP
+#define GPSIG_YG_DP 6
+#endif
+  static constexpr bool YG = DP >= GPSIG_YG_DP;
+  static constexpr int YR = YG ? 1 : W2;
+  f2 y[YR][DP], dy[W2][DP], hdy[W2];
   f2 Eq[W2], kc[W2];  // expm1(q_ij), k(x_i, y_j)
   float kcR;          // next lane's kc of its first column
   bool valid_last;
   bool clo = false;   // every |c_ij| of the wave < EM1_LO_TAU: Ec by the cubic (bound_c)
+  const float *fyb;   // YG: the block's point records, this lane's first column, the last point
+  int jl0, jlast;
+
+  // point y_j of column pair w2 (both halves), channel k
+  GPSIG_DEV f2 yv(int w2, int k) const {
+    if (!YG || w2 < YR) return y[w2 < YR ? w2 : 0][k];
+    f2 v;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int j = jl0 + w2 + h * W2;
+      v[h] = fyb[(long long)(j < jlast ? j : jlast) * FS + k];
+    }
+    return v;
+  }
 
   GPSIG_DEV void init(const float *__restrict__ fx, const float *__restrict__ fy, int gl, int l2) {
     const int ncols = l2 - 1;
+    fyb = fy;
+    jl0 = gl * W;
+    jlast = l2 - 1;
     // columns past the sequence clamp to its last point (zero increment): their cells are exact
     // zeros in the product form; only the lane's last column can see a foreign right neighbour.
     // l2 = points of this column block (its last one the halo point when the block is not the last)
@@ -264,7 +290,7 @@ struct RbfSeedPk {
         const bool cell = j < ncols;
 #pragma unroll
         for (int k = 0; k < DP; ++k) {
-          y[w2][k][h] = f[k];
+          if (w2 < YR) y[w2 < YR ? w2 : 0][k][h] = f[k];
           dy[w2][k][h] = cell ? f[DP + k] : 0.0f;
         }
         hdy[w2][h] = cell ? f[2 * DP] : 0.0f;
@@ -297,7 +323,7 @@ struct RbfSeedPk {
       f2 s = splat2(0.0f), qq = -hdy[w2];
 #pragma unroll
       for (int k = 0; k < DP; ++k) {
-        const f2 df = splat2(x[k]) - y[w2][k];
+        const f2 df = splat2(x[k]) - yv(w2, k);
         s = fma2(df, df, s);
         qq = fma2(df, dy[w2][k], qq);
       }
@@ -353,7 +379,7 @@ struct RbfSeedPk {
         f2 a = splat2(-rd.g), cc = splat2(0.0f);
 #pragma unroll
         for (int k = 0; k < DP; ++k) {
-          a = fma2(y[w2][k], splat2(rd.dx[k]), a);
+          a = fma2(yv(w2, k), splat2(rd.dx[k]), a);
           cc = fma2(dy[w2][k], splat2(rd.dx[k]), cc);
         }
         p[w2] = a;
@@ -461,7 +487,7 @@ struct RbfSeedPk {
       f4 accp = __builtin_amdgcn_mfma_f32_4x4x1f32(ng, 1.0f, zero, 0, 0, 0);
       f4 accq = __builtin_amdgcn_mfma_f32_4x4x1f32(ax[0], dy[w2][0][h], zero, 0, 0, 0);
 #pragma unroll
-      for (int k = 0; k < DP; ++k) accp = __builtin_amdgcn_mfma_f32_4x4x1f32(ax[k], y[w2][k][h], accp, 0, 0, 0);
+      for (int k = 0; k < DP; ++k) accp = __builtin_amdgcn_mfma_f32_4x4x1f32(ax[k], yv(w2, k)[h], accp, 0, 0, 0);
 #pragma unroll
       for (int k = 1; k < DP; ++k) accq = __builtin_amdgcn_mfma_f32_4x4x1f32(ax[k], dy[w2][k][h], accq, 0, 0, 0);
       P[w] = accp;

@@ -25,11 +25,16 @@ namespace gpsig {
 // per batch, instead of packed VALU dots.
 // SPLIT (diagnostic, SURVEY.md 8d "split design"): 1 = producer (cells dM of every row to p.dmbuf, no
 // recursion, no output), 2 = consumer (cells streamed from p.dmbuf through the recursion and epilogue).
+// Waves per SIMD the register allocation must leave room for: 2 (256 VGPRs) where W = 8 columns per lane
+// only just fit at D = 7..8 (the allocator would otherwise take 260 and run one wave per SIMD, 1.6x
+// slower; at 256 it spills a few registers outside the row loop).
+__host__ __device__ constexpr int fo_waves(int DP, int W, int M) { return (W == 8 && DP > 6 && M <= 6) ? 2 : 1; }
+
 template <int DP, int W, int LP, int M, int SEED, bool DIAGK, bool SAVE = false, bool MF = false, int SPLIT = 0>
 #ifdef GPSIG_FO_LB
 #define GPSIG_FO_BOUNDS __launch_bounds__(256, GPSIG_FO_LB)
 #else
-#define GPSIG_FO_BOUNDS __launch_bounds__(256)
+#define GPSIG_FO_BOUNDS __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(fo_waves(DP, W, M))))
 #endif
 __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
   using Seed = RowSeed<DP, W, SEED>;
@@ -303,11 +308,12 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
 // lane (more lanes per pair): W*DP <= 64 keeps the kernel within 256 VGPRs.
 struct Geo { int W, LP; };
 // W = 8 only while the kernel stays within 256 VGPRs (no AGPR spill): measured on MI355X with
-// tools/kbench.hip, W = 8 / LP = 16 beats W = 4 / LP = 32 by 8-18 % when it fits (D <= 5, any M;
-// D = 6, M <= 5) and loses 30-50 % when it does not (D = 6, M = 7: 49.4 vs 37.8 ms; D = 8, M = 6:
-// 220 vs 149 ms at N = 4096).
+// tools/kbench.hip, W = 8 / LP = 16 beats W = 4 / LP = 32 by 8-18 % when it fits and loses 30-50 % when
+// it does not.  With the points of column pairs >= 1 re-read on anchor rows (RbfSeedPk::YG, D >= 6) it
+// fits at D = 6 for every M (244-252 VGPRs) and at D = 7..8 for M <= 6 with fo_waves = 2 (D = 8, M = 6,
+// N = 4096: 145.4 -> 130.9 ms).
 __host__ __device__ constexpr int fo_wmax(int DP, int M) {
-  return DP <= 5 ? 8 : (DP <= 6 ? (M <= 5 ? 8 : 4) : (DP <= 16 ? 4 : 2));
+  return DP <= 6 ? 8 : (DP <= 8 ? (M <= 6 ? 8 : 4) : (DP <= 16 ? 4 : 2));
 }
 // Sequences longer than 64 * fo_wmax points run at LP = 64, W = fo_wmax in column blocks
 // (sig_fo_kernel, `nblk`), with one float per row and level of carry in LDS per wave.

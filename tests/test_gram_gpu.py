@@ -251,3 +251,23 @@ def test_empty_and_single_sequence_batches():
         got = kk.K(torch.as_tensor(X.reshape(n, -1), device=DEV), return_levels=True).cpu().numpy()
         exp = rr.K(X.reshape(n, -1), return_levels=True)
         np.testing.assert_allclose(got, exp, rtol=1e-5, atol=1e-6)
+
+
+@pytest.mark.parametrize("scale,jumps,D", [(0.02, False, 3), (0.15, False, 3), (0.05, True, 3), (0.03, True, 8)])
+def test_seed_regimes(scale, jumps, D):
+    """The RBF seed's regimes (sig_common.h RbfSeedPk::row) vs the oracle: small increments (expm1(c) by
+    the cubic under the |dx||dy| < 1/16 bound), medium ones (bound fails: the quintic), and rows with a few
+    large jumps (slow rows: cells outside the polynomial range take the corner difference, the in-range
+    cells after them re-evaluate their chained expm1(p)); D = 8 re-reads the points of column pairs >= 1
+    on anchor rows (YG)."""
+    import gpsig_amd
+    rng = np.random.default_rng(11)
+    N, L, M = 24, 40, 4
+    inc = rng.standard_normal((N, L, D)) * scale
+    if jumps:
+        inc[:, ::9, :] *= 25.0
+    X = np.cumsum(inc, 1)
+    k = gpsig_amd.SignatureRBF(L * D, D, M)
+    got = k.K(t(X.reshape(N, -1)), return_levels=True).cpu().numpy()
+    exp = kr.SignatureKernelRef(L * D, D, M).K(X.reshape(N, -1), return_levels=True)
+    assert (norm_rel_err(got, exp, axis_levels=True) < TOL).all()
