@@ -249,8 +249,10 @@ def main():
                      # the fused kernel never materialises the tile: physically it is VALU-issue bound
                      "physical_bound": "valu", "valu_busy": prof.get("valu_busy"),
                      "profile": os.path.relpath(args.traffic_json, ROOT) if prof else None,
-                     # the datasheet peak and a measured device-to-device copy, both
-                     "peak_probe": probe, "frac_probe": achieved / probe if probe else None},
+                     # the datasheet peak and a measured device-to-device copy (read + write
+                     # GB/s).  No fraction against the probe: `achieved` is an effective bandwidth of
+                     # algorithmic bytes the fused kernel never moves, so a ratio to a copy is meaningless.
+                     "peak_probe": probe},
     }
     if rank == 0 and not args.no_check:
         # parity on a bounded subsample: the normalised Gram restricted to a subset S of the sequences
