@@ -196,14 +196,18 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
 #pragma unroll
       for (int w2 = 0; w2 < W2; ++w2) C[0][w2] += dM[w2];
     };
-    // Row loop.  For the packed RBF seed the row recurrences are re-anchored every ANCHOR rows (a
-    // wave-uniform branch); the other seeds evaluate every row directly.
+    // Row loop.  For the packed RBF seed the row recurrences are re-anchored every ANCH rows (a
+    // wave-uniform branch); the other seeds evaluate every row directly.  The saved-state launch of a
+    // training step uses the same period, so it writes the inference launch's Gram bit for bit (the
+    // VJP, which regenerates its cells from an exact row every 4 rows, inverts the saved sums with
+    // cells that differ from these by the recurrences' rounding drift, ~1e-7 relative).
+    constexpr int ANCH = PSeed::ANCHOR;
 #ifndef GPSIG_FO_UNROLL2
 #define GPSIG_FO_UNROLL2 (W <= 4)
 #endif
     int i = 0;
     if constexpr (PK && MF) {
-      static_assert(PSeed::ANCHOR % 4 == 0, "anchor period");
+      static_assert(ANCH % 4 == 0, "anchor period");
       for (; i + 4 <= nrows; i += 4) {
         f4 P[W], Q[W];
         seed.mfma_pc(fx, i, P, Q);
@@ -217,7 +221,7 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
             pc[w2] = (f2){P[w2][r], P[w2 + W2][r]};
             pc[W2 + w2] = (f2){Q[w2][r], Q[w2 + W2][r]};
           }
-          do_row(std::false_type{}, i + r, rd, r == 3 && ((i + 3) % PSeed::ANCHOR) == PSeed::ANCHOR - 1, pc);
+          do_row(std::false_type{}, i + r, rd, r == 3 && ((i + 3) % ANCH) == ANCH - 1, pc);
         }
       }
     }
@@ -225,13 +229,13 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
     auto run_rows = [&](auto clo_t) {
       if constexpr (PK && GPSIG_FO_UNROLL2 && !MF) {
         // row pairs: ANCHOR is even, so the first row of a pair never anchors (compile-time)
-        static_assert(PSeed::ANCHOR % 2 == 0, "anchor period");
+        static_assert(ANCH % 2 == 0, "anchor period");
         for (; i + 2 <= nrows; i += 2) {
           Rec r0, r1;
           r0.load(fx, i);
           r1.load(fx, i + 1);
           do_row(clo_t, i, r0, false);
-          do_row(clo_t, i + 1, r1, ((i + 1) % PSeed::ANCHOR) == PSeed::ANCHOR - 1);
+          do_row(clo_t, i + 1, r1, ((i + 1) % ANCH) == ANCH - 1);
         }
       }
       for (; i < nrows; ++i) {
@@ -239,7 +243,7 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
         bool anch = true;
         if constexpr (PK) {
           rd.load(fx, i);
-          anch = (i % PSeed::ANCHOR) == PSeed::ANCHOR - 1;
+          anch = (i % ANCH) == ANCH - 1;
         } else {
           rd.load(fx, i, SEED);
         }
