@@ -10,7 +10,7 @@
 // and with increments (component = (z0, z1), seed = time difference of k(z1, x) - k(z0, x)):
 //   M = k(z0, x_s) (Ep Eq + (1 + Ep)(1 + Eq) Ec),  p = -<z0 - x_s, dz> - |dz|^2/2,  q = <z0, dx_s> - g_s,
 //   c = <dz, dx_s>;   k(z0, x_{s+1}) = k(z0, x_s)(1 + Eq),  Ep_{s+1} = Ep + Ec + Ep Ec.
-// k (and Ep) are re-evaluated exactly every ANCHOR cells.  Arguments past the polynomial range take
+// k (and Ep) are re-evaluated exactly every ANCHOR (32) cells.  Arguments past the polynomial range take
 // expm1 = e^x - 1 (a wave-uniform branch); with increments, |q| or |c| >= 2 (far-apart corners) takes
 // the plain corner difference of directly evaluated base-kernel values.
 #include "sig_common.h"
@@ -65,7 +65,10 @@ template <int DP, int M, bool INCR>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(INCR ? GPSIG_TVS_WPE : GPSIG_TVS_WPE0))) void tvs_pk_kernel(TvsPkArgs a) {
   constexpr int LT = M * (M + 1) / 2;
   constexpr int ZS = tvs_zs<DP, INCR>();
-  constexpr int ANCHOR = 8;
+#ifndef GPSIG_TVS_ANCHOR
+#define GPSIG_TVS_ANCHOR 32
+#endif
+  constexpr int ANCHOR = GPSIG_TVS_ANCHOR;
   constexpr float TVS_CORNER = 2.0f;  // |q| or |c| past this: corner form (increments)
   constexpr float NHL2E = -0.72134752044448170f, L2E = 1.4426950408889634f;
   const int lane = threadIdx.x;
