@@ -46,7 +46,7 @@ template <int DP, bool INCR>
 constexpr int tvs_bwd_chunk() { return DP > 8 ? 2 : (INCR ? 8 : 4); }
 
 // reverse-sweep steps between exact point values of the RBF difference cells (backward recurrence)
-constexpr int TVSB_ANCHOR = 8;
+constexpr int TVSB_ANCHOR = 32;
 
 // Level I only (levels are independent chains; blockIdx.z selects the level, so the per-lane state is
 // O(I * DP) and not O(M^2 * DP)).  LT below is the number of components of this level.
