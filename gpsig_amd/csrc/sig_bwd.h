@@ -190,7 +190,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
   constexpr bool RBF = (SEED == SEED_RBF_DIFF || SEED == SEED_RBF_POINT);   // base kernel
   constexpr float NHL2E = -0.72134752044448170f;  // exp(-d2/2) = exp2(d2 * NHL2E)
   constexpr float L2E = 1.4426950408889634f;
-  constexpr int RC = W >= 4 ? 4 : 8;  // rows per chunk of the reverse sweep (<= the forward's anchor period)
+#ifndef GPSIG_BWD_RC
+#define GPSIG_BWD_RC 4
+#endif
+  // rows per chunk of the reverse sweep (LDS: 4 waves x RC x 64 lanes x 2W floats per workgroup)
+  constexpr int RC = W >= 4 ? GPSIG_BWD_RC : 8;
   __shared__ __attribute__((aligned(16))) float cbuf[RBF && DIFF ? 4 : 1][RBF && DIFF ? RC : 1][64][2 * W];
   __shared__ float tbuf[DP <= 8 ? 4 : 1][DP <= 8 ? 4 : 1][DP <= 8 ? DP : 1][64];  // x-gradient row batches
   constexpr int ML = M > 1 ? M - 1 : 1;
