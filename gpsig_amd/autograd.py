@@ -193,7 +193,7 @@ class TensVsSeq(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gout):
         cfg = ctx.cfg
-        _check_bwd(cfg, gram=True)
+        _check_bwd(cfg)  # gpsig_tens_vs_seq_vjp differentiates the order-1 recursion only
         Zs, Xs = ctx.saved_tensors
         gZ, gX = ops.tens_vs_seq_vjp(Zs.detach(), Xs.detach(), cfg["num_levels"], gout, cfg["base"],
                                      cfg["increments"], difference=cfg["difference"], state=ctx.state)

@@ -1,11 +1,14 @@
 // gpsig_amd -- extern "C" entry points (include/gpsig_amd.h): argument checks, workspace carving,
 // tile counts, and dispatch to the templated kernels.  No allocation, no synchronisation.
 #include "sig_common.h"
+#include "wide.h"
+
+#include <stdlib.h>
 
 namespace gpsig {
 int features(const float *X, int n, int l, int d, int DP, float *F, hipStream_t s);
 int sig_fo_launch(const SigArgs &a, int DP, int seed, long long nblocks, hipStream_t s);
-int fo_lanes_per_pair(int l2, int DP, int M, bool mf);
+int fo_lanes_per_pair(int l2, int DP, int M, bool mf, int seed);
 size_t fo_split_bytes(int l1, int l2, int DP, int M);
 int sig_ho_launch(const SigArgs &a, int DP, int seed, long long nblocks, hipStream_t s);
 int ho_lanes_per_pair(int l2, int order, int M);
@@ -31,10 +34,20 @@ static int pad_channels(int d, int order) {
 
 static size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 
+// Channel counts past the fixed instantiations run the first-order kernels on channel-major records
+// with a runtime channel loop (wide.h)
+// (GPSIG_FO_FIXED_MAX pins the crossover for A/B runs: 0 sends every channel count to the wide kernels)
+static int fo_fixed_max() {
+  static const int v = [] { const char *e = getenv("GPSIG_FO_FIXED_MAX"); return e ? atoi(e) : 32; }();
+  return v;
+}
+static bool wide_channels(int d, int order) { return order == 1 && d > fo_fixed_max(); }
+
 static size_t feat_bytes(int n, int l, int d) {
+  const size_t wb = d > fo_fixed_max() ? align256((size_t)n * wide_rec_floats(d, l) * sizeof(float)) : 0;
   const int DP = pad_channels(d, 2);  // the wider of the two paddings
-  if (DP == 0) return 0;
-  return align256((size_t)n * l * feat_stride(DP) * sizeof(float));
+  const size_t fb = DP ? align256((size_t)n * l * feat_stride(DP) * sizeof(float)) : 0;
+  return wb > fb ? wb : fb;
 }
 
 static int seed_of(int base_kind, int difference) {
@@ -77,21 +90,23 @@ static int sig_gram_impl(const float *X, int n1, int l1, const float *Y, int n2,
   if (mfma && (seed != SEED_RBF_DIFF || order != 1 || state)) return GPSIG_EUNSUPPORTED;
   if (split && (mfma || seed != SEED_RBF_DIFF || order != 1 || state || pair_mode == GPSIG_PAIRS_DIAG))
     return GPSIG_EUNSUPPORTED;
-  const int DP = pad_channels(d, order);
-  if (seed < 0 || DP == 0) return GPSIG_EUNSUPPORTED;
+  const bool wide = wide_channels(d, order);
+  const int DP = wide ? 0 : pad_channels(d, order);
+  if (seed < 0 || (DP == 0 && !wide)) return GPSIG_EUNSUPPORTED;
+  if (wide && (mfma || split)) return GPSIG_EUNSUPPORTED;
   if (row_end == row_begin) return GPSIG_OK;
 
   const bool same = (X == Y && n1 == n2 && l1 == l2);
-  const size_t fx_b = align256((size_t)n1 * l1 * feat_stride(DP) * sizeof(float));
-  const size_t fy_b = same ? 0 : align256((size_t)n2 * l2 * feat_stride(DP) * sizeof(float));
+  const size_t fx_b = wide ? feat_bytes(n1, l1, d) : align256((size_t)n1 * l1 * feat_stride(DP) * sizeof(float));
+  const size_t fy_b = same ? 0 : (wide ? feat_bytes(n2, l2, d) : align256((size_t)n2 * l2 * feat_stride(DP) * sizeof(float)));
   const size_t dm_b = split ? gpsig_sig_split_bytes(l1, l2, d, num_levels) : 0;
   if (split && dm_b == 0) return GPSIG_EUNSUPPORTED;
   if (!workspace || workspace_bytes < fx_b + fy_b + dm_b) return GPSIG_EWORKSPACE;
   float *FX = static_cast<float *>(workspace);
   float *FY = same ? FX : reinterpret_cast<float *>(static_cast<char *>(workspace) + fx_b);
-  int rc = features(X, n1, l1, d, DP, FX, s);
+  int rc = wide ? wide_records(X, n1, l1, d, FX, s) : features(X, n1, l1, d, DP, FX, s);
   if (rc) return rc;
-  if (!same && (rc = features(Y, n2, l2, d, DP, FY, s))) return rc;
+  if (!same && (rc = wide ? wide_records(Y, n2, l2, d, FY, s) : features(Y, n2, l2, d, DP, FY, s))) return rc;
 
   SigArgs a{};
   a.FX = FX;
@@ -114,8 +129,13 @@ static int sig_gram_impl(const float *X, int n1, int l1, const float *Y, int n2,
   a.state = state;
   a.mfma = mfma ? 1 : 0;
   a.dmbuf = split ? reinterpret_cast<float *>(static_cast<char *>(workspace) + fx_b + fy_b) : nullptr;
+  a.wd = d;
+  a.lw1 = wide_lw(l1);
+  a.lw2 = wide_lw(l2);
+  a.sx = wide_rec_floats(d, l1);
+  a.sy = wide_rec_floats(d, l2);
 
-  const int LP = (order == 1) ? fo_lanes_per_pair(l2, DP, num_levels, mfma) : ho_lanes_per_pair(l2, order, num_levels);
+  const int LP = (order == 1) ? fo_lanes_per_pair(l2, DP, num_levels, mfma, seed) : ho_lanes_per_pair(l2, order, num_levels);
   if (LP == 0) return GPSIG_EUNSUPPORTED;
   const int G = 64 / LP;
   long long nblocks = 0;

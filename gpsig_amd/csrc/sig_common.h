@@ -42,6 +42,10 @@ struct SigArgs {
   // chunked launch, dmbuf slot of a pair = its workgroup-local index
   float *dmbuf;
   long long blk0;
+  // wide channel counts (DP == 0 instantiations, wide.h): channel count, padded record lengths and
+  // record strides (floats) of X and Y
+  int wd, lw1, lw2;
+  long long sx, sy;
 };
 
 // Saved forward state of a first-order pair (gpsig_sig_gram_state): column sums of levels 1..M-1

@@ -15,8 +15,15 @@
 #include <type_traits>
 
 #include "sig_common.h"
+#include "wide.h"
 
 namespace gpsig {
+
+// Rows per channel-loop chunk of the wide-channel seeds (DP == 0, wide.h)
+#ifndef GPSIG_WIDE_R
+#define GPSIG_WIDE_R 4
+#endif
+constexpr int WIDE_R = GPSIG_WIDE_R;
 
 // DIAGK: the diagonal pass (pairs (a, a)) is the same body under its own symbol, so profiler
 // statistics of the Gram launch are not mixed with it.  SAVE: also write the VJP's saved state
@@ -28,6 +35,14 @@ namespace gpsig {
 // Waves per SIMD the register allocation must leave room for: 2 (256 VGPRs) where W = 8 columns per lane
 // only just fit at D = 7..8 (the allocator would otherwise take 260 and run one wave per SIMD, 1.6x
 // slower; at 256 it spills a few registers outside the row loop).
+// per-row record type of the row loop: the seed's own (wide, packed RBF) or the generic RowData
+template <bool WIDE, bool PK, class PS, int DP, int W>
+struct FoRec { using type = RowData<DP>; };
+template <bool PK, class PS, int DP, int W>
+struct FoRec<true, PK, PS, DP, W> { using type = typename PS::Row; };
+template <class PS, int DP, int W>
+struct FoRec<false, true, PS, DP, W> { using type = typename RbfSeedPk<DP, W>::Row; };
+
 __host__ __device__ constexpr int fo_waves(int DP, int W, int M) { return (W == 8 && DP > 6 && M <= 6) ? 2 : 1; }
 
 template <int DP, int W, int LP, int M, int SEED, bool DIAGK, bool SAVE = false, bool MF = false, int SPLIT = 0>
@@ -37,7 +52,9 @@ template <int DP, int W, int LP, int M, int SEED, bool DIAGK, bool SAVE = false,
 #define GPSIG_FO_BOUNDS __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(fo_waves(DP, W, M))))
 #endif
 __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
-  using Seed = RowSeed<DP, W, SEED>;
+  // DP == 0: wide channel counts (runtime p.wd, channel-major records, wide.h)
+  constexpr bool WIDE = DP == 0;
+  constexpr bool DIFF = SEED == SEED_RBF_DIFF || SEED == SEED_LIN_DIFF;
   constexpr int FS = feat_stride(DP);
   constexpr int G = 64 / LP;
 
@@ -68,6 +85,7 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
     if (a < p.row_begin || a >= p.row_end) return;  // wave-uniform
   }
   static_assert(SPLIT == 0 || (!DIAGK && !SAVE && !MF && SEED == SEED_RBF_DIFF), "split: RBF Gram pairs only");
+  static_assert(!WIDE || (SPLIT == 0 && !MF), "wide channels: fused VALU seed");
   // split: this pair's cell slab, [row][lane of the group][W] (each lane's W cells contiguous)
   float *__restrict__ dms = nullptr;
   if constexpr (SPLIT != 0)
@@ -77,14 +95,15 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
   if (DIAGK) pair_ok = (g == 0);
   const int bl = b < p.n2 ? b : p.n2 - 1;
 
-  const float *__restrict__ fx = p.FX + (long long)a * p.l1 * FS;
-  const float *__restrict__ fy = p.FY + (long long)bl * p.l2 * FS;
+  const float *__restrict__ fx = p.FX + (WIDE ? (long long)a * p.sx : (long long)a * p.l1 * FS);
+  const float *__restrict__ fy = p.FY + (WIDE ? (long long)bl * p.sy : (long long)bl * p.l2 * FS);
 
-  constexpr bool PK = (SEED == SEED_RBF_DIFF);
-  using PSeed = std::conditional_t<PK, RbfSeedPk<DP, W>, RowSeed<DP, W, SEED>>;
+  constexpr bool PK = (SEED == SEED_RBF_DIFF) && !WIDE;
+  using PSeed = std::conditional_t<WIDE, WideSeed<W, WIDE_R, SEED>,
+                                   std::conditional_t<PK, RbfSeedPk<DP, W>, RowSeed<DP, W, SEED>>>;
   constexpr int W2 = W / 2;
   constexpr int ML = M > 1 ? M - 1 : 1;
-  const int nrows = Seed::DIFF ? p.l1 - 1 : p.l1;
+  const int nrows = DIFF ? p.l1 - 1 : p.l1;
 
   // Column blocks (sequences longer than one lane group covers, LP = 64 only): block k holds the
   // cells j0 .. j0 + CPB - 1 (j0 = k CPB) on the points j0 .. j0 + CPB (the last lane's last column is
@@ -104,13 +123,17 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
   for (int blk = 0; blk < nblk; ++blk) {
     const int j0 = blk * CPB;
     // points of this block: the DIFF seeds see the halo point, the point seeds do not
-    const int npts = nblk == 1 ? p.l2 : min(p.l2 - j0, Seed::DIFF ? CPB + 1 : CPB);
+    const int npts = nblk == 1 ? p.l2 : min(p.l2 - j0, DIFF ? CPB + 1 : CPB);
     PSeed seed;
-    seed.init(fx, fy + (long long)j0 * FS, gl, npts);
+    if constexpr (WIDE)
+      seed.init(p.wd, p.lw2, fx, fy + j0, gl, npts);
+    else
+      seed.init(fx, fy + (long long)j0 * FS, gl, npts);
 #ifndef GPSIG_CLO
 #define GPSIG_CLO 1
 #endif
     if constexpr (PK && !MF && SPLIT != 2 && GPSIG_CLO) seed.bound_c(fx, nrows);
+    if constexpr (WIDE && SEED == SEED_RBF_DIFF && GPSIG_CLO) seed.bound_c(nrows);
 
     f2 C[M][W2];
 #pragma unroll
@@ -120,7 +143,7 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
 
     // One row: seed cells, then the level recursion.  S_m = exclusive prefix over (rows < i, cols < j)
     // of R_m = exclusive scan over j of C_m; the M-1 scans are independent and interleave.
-    using Rec = std::conditional_t<PK, typename RbfSeedPk<DP, W>::Row, RowData<DP>>;
+    using Rec = typename FoRec<WIDE, PK, PSeed, DP, W>::type;
     auto do_row = [&](auto clo_t, int i, const Rec &rd, bool anch, const f2 *pc = nullptr) {
       f2 dM[W2];
       if constexpr (SPLIT == 2) {
@@ -131,6 +154,8 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
           dM[2 * w4] = (f2){v[0], v[1]};
           dM[2 * w4 + 1] = (f2){v[2], v[3]};
         }
+      } else if constexpr (WIDE) {
+        seed.template row<decltype(clo_t)::value>(rd, anch, dM);
       } else if constexpr (PK) {
         if (MF && pc) {
           f2 pp[W2], cc[W2];
@@ -227,6 +252,27 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
     }
     // the rest of the rows, in a copy per Ec polynomial (the pair block's |c| bound, bound_c)
     auto run_rows = [&](auto clo_t) {
+      if constexpr (WIDE) {
+        // chunks of WIDE_R rows: one channel loop for their dots, then the rows (compile-time slots)
+        for (; i < nrows; i += WIDE_R) {
+          seed.chunk(i);
+          auto one = [&](auto rr) {
+            constexpr int r = decltype(rr)::value;
+            if (i + r < nrows) {
+              const Rec rd = seed.template row_of<r>(i + r);
+              do_row(clo_t, i + r, rd, ((i + r) % ANCH) == ANCH - 1);
+            }
+          };
+          one(std::integral_constant<int, 0>{});
+          if constexpr (WIDE_R > 1) one(std::integral_constant<int, 1>{});
+          if constexpr (WIDE_R > 2) one(std::integral_constant<int, 2>{});
+          if constexpr (WIDE_R > 3) one(std::integral_constant<int, 3>{});
+          if constexpr (WIDE_R > 4) one(std::integral_constant<int, 4>{});
+          if constexpr (WIDE_R > 5) one(std::integral_constant<int, 5>{});
+          if constexpr (WIDE_R > 6) one(std::integral_constant<int, 6>{});
+          if constexpr (WIDE_R > 7) one(std::integral_constant<int, 7>{});
+        }
+      } else {
       if constexpr (PK && GPSIG_FO_UNROLL2 && !MF) {
         // row pairs: ANCHOR is even, so the first row of a pair never anchors (compile-time)
         static_assert(ANCH % 2 == 0, "anchor period");
@@ -249,8 +295,9 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
         }
         do_row(clo_t, i, rd, anch);
       }
+      }
     };
-    if constexpr (PK && !MF && SPLIT != 2) {
+    if constexpr ((PK && !MF && SPLIT != 2) || (WIDE && SEED == SEED_RBF_DIFF)) {
       if (seed.clo)
         run_rows(std::true_type{});
       else
@@ -261,7 +308,7 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
 
     // ---- saved VJP state (gpsig_sig_gram_state): column sums of levels 1..M-1 (column pair k holds
     // columns k, k + W/2), before the epilogue so it adds no live registers there
-    static_assert(!SAVE || (!DIAGK && Seed::DIFF), "saved state: Gram pairs of a DIFF seed");
+    static_assert(!SAVE || (!DIAGK && DIFF), "saved state: Gram pairs of a DIFF seed");
     if constexpr (SAVE) {
       if (pair_ok) {
         const int nc = p.l2 - 1;
@@ -296,7 +343,12 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
 #pragma unroll
   for (int m = 0; m < M; ++m) K[m + 1] = Kacc[m];
   if (gl == 0 && pair_ok) {
-    if constexpr (Seed::DIFF) K[1] = level1_closed<DP, SEED>(fx, fy, p.l1, p.l2);
+    if constexpr (DIFF) {
+      if constexpr (WIDE)
+        K[1] = level1_closed_wide<SEED>(fx, fy, p.wd, p.lw1, p.lw2, p.l1, p.l2);
+      else
+        K[1] = level1_closed<DP, SEED>(fx, fy, p.l1, p.l2);
+    }
     store_pair<M>(p, a, b, K);
     if constexpr (SAVE) {  // raw levels K_1..K_M after the column sums
       float *__restrict__ st = p.state + state_slot(a, b, p.n2, p.pair_mode == GPSIG_PAIRS_UPPER) * state_stride(M, p.l2) +
@@ -321,6 +373,13 @@ __host__ __device__ constexpr int fo_wmax(int DP, int M) {
 }
 // Sequences longer than 64 * fo_wmax points run at LP = 64, W = fo_wmax in column blocks
 // (sig_fo_kernel, `nblk`), with one float per row and level of carry in LDS per wave.
+// Wide channels (DP == 0): no column data in registers, W = 8 from 65 points on (W = 4 below, RBF only).
+inline Geo fo_geometry_wide(int l2, int seed) {
+  if (l2 <= 64 && seed == SEED_RBF_DIFF) return {4, 16};
+  for (int LP : {16, 32, 64})
+    if (LP * 8 >= l2) return {8, LP};
+  return {8, 64};
+}
 inline Geo fo_geometry(int l2, int DP, int M, bool mf = false) {
   if (mf) {  // matrix-core seed (RBF difference seed only): W = 4 columns per lane, no column blocks
     for (int LP : {16, 32, 64})
@@ -387,8 +446,22 @@ int launch_fo_split(const SigArgs &a0, long long nblocks, hipStream_t s) {
   }
 }
 
+template <int M, int SEED>
+int fo_geo_wide(const SigArgs &a, long long nblocks, hipStream_t s) {
+  if (a.mfma || a.dmbuf) return GPSIG_EUNSUPPORTED;
+  const Geo geo = fo_geometry_wide(a.l2, SEED);
+  if constexpr (SEED == SEED_RBF_DIFF)
+    if (geo.W == 4) return launch_fo<0, 4, 16, M, SEED>(a, nblocks, s);
+  if (geo.LP == 16) return launch_fo<0, 8, 16, M, SEED>(a, nblocks, s);
+  if (geo.LP == 32) return launch_fo<0, 8, 32, M, SEED>(a, nblocks, s);
+  return launch_fo<0, 8, 64, M, SEED>(a, nblocks, s);
+}
+
 template <int DP, int M, int SEED>
 int fo_geo(const SigArgs &a, long long nblocks, hipStream_t s) {
+  if constexpr (DP == 0) {  // wide channel counts
+    return fo_geo_wide<M, SEED>(a, nblocks, s);
+  } else {
   const Geo geo = fo_geometry(a.l2, DP, M, a.mfma != 0);
   if constexpr (SEED == SEED_RBF_DIFF) {
     if (a.mfma) {  // A/B variant: seed dots on the matrix cores (not for the saved-state launch)
@@ -418,6 +491,7 @@ int fo_geo(const SigArgs &a, long long nblocks, hipStream_t s) {
   if constexpr (WM >= 8) { GPSIG_GEO(8, 16) GPSIG_GEO(8, 32) GPSIG_GEO(8, 64) }
 #undef GPSIG_GEO
   return GPSIG_EUNSUPPORTED;
+  }
 }
 
 // sig_fo_launch_dpm<DP, M> (the per-seed dispatch) is defined only in sig_fo_inst.hip, one translation

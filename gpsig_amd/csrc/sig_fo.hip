@@ -79,20 +79,53 @@ static int fo_dp(const SigArgs &a, int seed, long long nblocks, hipStream_t s) {
 }
 
 int sig_fo_launch(const SigArgs &a0, int DP, int seed, long long nblocks, hipStream_t s) {
-  const Geo g = fo_geometry(a0.l2, DP, a0.M, a0.mfma != 0);
+  const Geo g = DP == 0 ? fo_geometry_wide(a0.l2, seed) : fo_geometry(a0.l2, DP, a0.M, a0.mfma != 0);
   if (g.W == 0) return GPSIG_EUNSUPPORTED;
   SigArgs a = a0;
   a.nblk = fo_blocks(a0.l2, seed == SEED_RBF_DIFF || seed == SEED_LIN_DIFF, g);
   switch (DP) {
 #define CASE(v) \
   case v: return fo_dp<v>(a, seed, nblocks, s);
-    CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(8) CASE(16) CASE(32)
+    CASE(0) CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(8) CASE(16) CASE(32)
 #undef CASE
     default: return GPSIG_EUNSUPPORTED;
   }
 }
 
-int fo_lanes_per_pair(int l2, int DP, int M, bool mf) { return fo_geometry(l2, DP, M, mf).LP; }
+int fo_lanes_per_pair(int l2, int DP, int M, bool mf, int seed) {
+  return (DP == 0 ? fo_geometry_wide(l2, seed) : fo_geometry(l2, DP, M, mf)).LP;
+}
+
+// ------------------------------------------------------------------------------------ wide records
+__global__ __launch_bounds__(256) void wide_records_kernel(const float *__restrict__ X, int n, int l, int d,
+                                                           float *__restrict__ R) {
+  const int lw = wide_lw(l);
+  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= (long long)n * lw) return;
+  const int sq = (int)(idx / lw), j = (int)(idx % lw);
+  const int jj = j < l ? j : l - 1;
+  const bool inc = j + 1 < l;
+  const float *x = X + ((long long)sq * l + jj) * d;
+  float *r = R + (long long)sq * wide_rec_floats(d, l) + j;
+  float h = 0.0f;
+  double gx = 0.0;
+  for (int k = 0; k < d; ++k) {
+    const float xv = x[k];
+    const float dv = inc ? x[d + k] - xv : 0.0f;
+    r[(long long)k * lw] = xv;
+    r[(long long)(d + k) * lw] = dv;
+    h = __builtin_fmaf(dv, dv, h);
+    gx = __builtin_fma((double)xv, (double)dv, gx);
+  }
+  r[(long long)2 * d * lw] = 0.5f * h;
+  r[(long long)(2 * d + 1) * lw] = (float)(gx + 0.5 * (double)h);
+}
+
+int wide_records(const float *X, int n, int l, int d, float *R, hipStream_t s) {
+  const long long tot = (long long)n * wide_lw(l);
+  hipLaunchKernelGGL(wide_records_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, X, n, l, d, R);
+  return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
+}
 
 // one chunk of the split diagnostic: FO_SPLIT_BLOCKS workgroups x 4 waves x G pairs, (l1 - 1) rows of
 // LP * W cells each (0: the geometry has column blocks or W < 4, where the split does not apply)

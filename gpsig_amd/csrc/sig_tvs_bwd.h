@@ -362,7 +362,9 @@ __device__ __forceinline__ void tvs_bwd_level(const TvsBwdArgs &a,
 #pragma unroll
           for (int q = 0; q < DP; ++q) qv = __builtin_fmaf(z0c(k, q), dx[q], qv);
           const float E = em1(qv);
-          if (anchor) pvals(k, x, c0v[k], c1v[k]);
+          // far from the polynomial range (|q| >= EM1_TAU in some lane) 1 + expm1(q) loses digits or
+          // underflows to 0 (q < -17.3): the step takes the exact point values instead (wave-uniform)
+          if (anchor || __builtin_amdgcn_ballot_w64(!(__builtin_fabsf(qv) < EM1_TAU)) != 0) pvals(k, x, c0v[k], c1v[k]);
           else c0v[k] = pv0[k] * __builtin_amdgcn_rcpf(1.0f + E);
           c1v[k] = 0.f;
           m[st] = c0v[k] * E;

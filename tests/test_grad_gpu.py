@@ -376,3 +376,44 @@ def test_tens_vs_seq_saved_state_vjp_equals_recompute(base, increments):
     gz1, gx1 = ops.tens_vs_seq_vjp(Z, X, M, G, base, increments, state=st)
     assert norm_rel_err(gz1.cpu().numpy(), gz0.cpu().numpy()) < 1e-5
     assert norm_rel_err(gx1.cpu().numpy(), gx0.cpu().numpy()) < 1e-5
+
+
+def test_tens_vs_seq_higher_order_backward_raises():
+    """K_tens_vs_seq of SignatureLinear(order=num_levels) runs the higher-order recursion forward
+    (signature_algs.py:129-160); gpsig_tens_vs_seq_vjp differentiates the order-1 recursion only, so the
+    backward must raise instead of returning the order-1 gradient."""
+    import gpsig_amd
+    M, D, L, T, N = 3, 2, 10, 3, 5
+    LT = M * (M + 1) // 2
+    rng = np.random.default_rng(70)
+    k = gpsig_amd.SignatureLinear(L * D, D, M, order=M)
+    Zt = torch.tensor(0.5 * rng.standard_normal((LT, T, D)), device=DEV, requires_grad=True)
+    Xt = torch.tensor(walks(N, L, D, 71).reshape(N, -1), device=DEV, requires_grad=True)
+    with pytest.raises(NotImplementedError):
+        k.K_tens_vs_seq(Zt, Xt).sum().backward()
+
+
+def test_tens_vs_seq_vjp_far_inducing_point():
+    """An inducing point about 10 lengthscales from the path with outward steps of ~1.7 drives
+    q = <z, dx_s> - g_s below -17, where 1 + expm1(q) underflows to 0 in fp32: the Kuf VJP's backward
+    recurrence of k(z, x_s) must take exact point values there (finite gradients, oracle parity)."""
+    import gpsig_amd
+    M, D, L, T, N = 3, 2, 24, 4, 9
+    LT = M * (M + 1) // 2
+    rng = np.random.default_rng(72)
+    X = np.cumsum(rng.standard_normal((N, L, D)) * 0.3, 1)
+    X[:, L // 2:, :] += np.linspace(0, 1.7 * (L - L // 2), L - L // 2)[None, :, None] * np.array([1.0, 0.0])
+    Z = rng.standard_normal((LT, T, D)) * 0.3
+    Z[:, 0, :] = [-10.0, 0.0]  # far on the other side of the path
+    G = rng.standard_normal((T, N))
+    k = gpsig_amd.SignatureRBF(L * D, D, M, normalization=False)
+    Zt = torch.tensor(Z, device=DEV, requires_grad=True)
+    Xt = torch.tensor(X.reshape(N, -1), device=DEV, requires_grad=True)
+    K = k.K_tens_vs_seq(Zt, Xt)
+    (K * torch.as_tensor(G, device=DEV)).sum().backward()
+    assert torch.isfinite(Zt.grad).all() and torch.isfinite(Xt.grad).all()
+    Zr, Xr = torch.tensor(Z, requires_grad=True), torch.tensor(X, requires_grad=True)
+    Kr = ar.K_tens_vs_seq(Zr, Xr, M, base="rbf", normalization=False)
+    (Kr * torch.tensor(G)).sum().backward()
+    assert norm_rel_err(Zt.grad.cpu().numpy(), Zr.grad.numpy()) < GTOL
+    assert norm_rel_err(Xt.grad.reshape(X.shape).cpu().numpy(), Xr.grad.numpy()) < GTOL

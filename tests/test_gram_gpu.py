@@ -171,15 +171,16 @@ def test_full_size_properties_headline():
     assert norm_rel_err(got, exp) < TOL
 
 
-@pytest.mark.parametrize("case", ["channels", "levels", "length"])
+@pytest.mark.parametrize("case", ["order", "levels", "length"])
 def test_unsupported_configurations_raise(case):
     """Configurations outside the compiled instantiations fail loudly (GpsigError), never silently."""
     import gpsig_amd
     from gpsig_amd import ops
-    D, M, L = {"channels": (40, 3, 10), "levels": (3, 9, 10), "length": (4, 3, 6000)}[case]  # LDS carry of the column blocks > 160 KiB
+    # order 9 > the higher-order kernel's 8; 9 levels; LDS carry of the column blocks > 160 KiB
+    D, M, L, order = {"order": (3, 10, 10, 9), "levels": (3, 9, 10, 1), "length": (4, 3, 6000, 1)}[case]
     X = torch.zeros((2, L, D), device=DEV)
     with pytest.raises(gpsig_amd.GpsigError):
-        ops.sig_gram(X, None, M)
+        ops.sig_gram(X, None, M, order=order)
 
 
 @pytest.mark.parametrize("L,D,M", [(20, 3, 4), (50, 5, 5), (100, 5, 5), (128, 8, 6), (200, 2, 3)])
