@@ -37,10 +37,12 @@ static size_t align256(size_t b) { return (b + 255) & ~(size_t)255; }
 // Channel counts past the fixed instantiations run the first-order kernels on channel-major records
 // with a runtime channel loop (wide.h)
 // (GPSIG_FO_FIXED_MAX pins the crossover for A/B runs: 0 sends every channel count to the wide kernels)
-static int fo_fixed_max() {
+namespace gpsig {
+int fo_fixed_max() {
   static const int v = [] { const char *e = getenv("GPSIG_FO_FIXED_MAX"); return e ? atoi(e) : 32; }();
   return v;
 }
+}  // namespace gpsig
 static bool wide_channels(int d, int order) { return order == 1 && d > fo_fixed_max(); }
 
 static size_t feat_bytes(int n, int l, int d) {

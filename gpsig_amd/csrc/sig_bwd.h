@@ -52,6 +52,14 @@ struct BwdArgs {
   long long blk0;  // first logical workgroup of this launch (the host splits blocked launches)
   float *scratch;
   long long scr_stride;
+  // wide channel counts (sig_bwd_wide.h): channel count, padded record lengths, record strides, and the
+  // point-weight tile of the launch: pair (a, b), point row i at tile + (a - tile_a0) tile_as +
+  // (b - tile_b0) l2 + i tile_ld (DIAG: + i tile_ld only)
+  int wd, lw1, lw2;
+  long long sx, sy;
+  float *tile;
+  int tile_a0, tile_b0;
+  long long tile_as, tile_ld;
 };
 
 // Load of a carry another lane of this wave stored earlier in the launch: served by L2 (agent scope),

@@ -5,6 +5,12 @@
 
 namespace gpsig {
 int features(const float *X, int n, int l, int d, int DP, float *F, hipStream_t s);
+int fo_fixed_max();
+size_t sig_bwd_wide_workspace(int n1, int l1, int n2, int l2, int d);
+int sig_bwd_wide(BwdArgs a, const float *X, const float *Y, int seed, void *workspace, size_t workspace_bytes,
+                 hipStream_t s);
+// channel counts past the VJP's instantiations (or past the forward's crossover): the wide-channel VJP
+static bool bwd_wide(int d) { return d > 16 || d > fo_fixed_max(); }
 template <int DP, int M>
 int sig_bwd_launch_dpm(const BwdArgs &a, int seed, long long nblocks, hipStream_t s);
 
@@ -66,10 +72,46 @@ extern "C" int gpsig_sig_gram_vjp(const float *X, int n1, int l1, const float *Y
   if (state && (pair_mode == GPSIG_PAIRS_DIAG || !difference)) return GPSIG_EINVAL;
   const int seed = base_kind == GPSIG_BASE_RBF ? (difference ? SEED_RBF_DIFF : SEED_RBF_POINT)
                    : base_kind == GPSIG_BASE_LINEAR ? (difference ? SEED_LIN_DIFF : SEED_LIN_POINT) : -1;
-  const int DP = bwd_pad(d);
-  if (seed < 0 || DP == 0) return GPSIG_EUNSUPPORTED;
+  const bool wide = bwd_wide(d);
+  const int DP = wide ? 0 : bwd_pad(d);
+  if (seed < 0 || (DP == 0 && !wide) || num_levels > 8) return GPSIG_EUNSUPPORTED;
+  if (wide) {
+    if (row_end == row_begin) return GPSIG_OK;
+    if (!workspace || workspace_bytes < GSC_BYTES + sig_bwd_wide_workspace(n1, l1, n2, l2, d)) return GPSIG_EWORKSPACE;
+    float *gsc_slots = static_cast<float *>(workspace);
+    BwdArgs a{};
+    a.n1 = n1; a.l1 = l1; a.n2 = n2; a.l2 = l2; a.d = d;
+    a.M = num_levels;
+    a.pair_mode = pair_mode;
+    a.row_begin = row_begin;
+    a.row_end = row_end;
+    a.gout = gout;
+    a.gout_levels = gout_levels ? 1 : 0;
+    a.g_ld = n2;
+    a.g_lvl = pair_mode == GPSIG_PAIRS_DIAG ? (long long)n1 : (long long)n1 * n2;
+    a.rs1 = rs1; a.rs2 = rs2; a.scale = scale;
+    a.jitter = jitter;
+    a.gX = gX;
+    a.gY = pair_mode == GPSIG_PAIRS_RECT ? gY : gX;
+    a.grs1 = grs1;
+    a.grs2 = pair_mode == GPSIG_PAIRS_RECT ? grs2 : grs1;
+    a.gscale = nullptr;
+    if (gscale && pair_mode != GPSIG_PAIRS_DIAG) {
+      if (hipMemsetAsync(gsc_slots, 0, GSC_BYTES, s) != hipSuccess) return GPSIG_ELAUNCH;
+      a.gscale = gsc_slots;
+    }
+    a.state = state;
+    const int rc = sig_bwd_wide(a, X, pair_mode == GPSIG_PAIRS_RECT ? Y : X, seed, static_cast<char *>(workspace) + GSC_BYTES,
+                                workspace_bytes - GSC_BYTES, s);
+    if (rc) return rc;
+    if (a.gscale) {
+      hipLaunchKernelGGL(gscale_reduce_kernel, dim3(1), dim3(64), 0, s, gsc_slots, num_levels + 1, gscale);
+      if (hipGetLastError() != hipSuccess) return GPSIG_ELAUNCH;
+    }
+    return GPSIG_OK;
+  }
   const BwdGeo geo = bwd_geometry(l2, DP);
-  if (geo.W == 0 || num_levels > 8) return GPSIG_EUNSUPPORTED;
+  if (geo.W == 0) return GPSIG_EUNSUPPORTED;
   if (row_end == row_begin) return GPSIG_OK;
   const int nblk = bwd_blocks(l2, difference != 0, geo);
   const long long scr_stride = bwd_scratch_floats(difference ? l1 - 1 : l1, num_levels, geo.W, nblk);
@@ -155,6 +197,8 @@ extern "C" int gpsig_sig_gram_vjp(const float *X, int n1, int l1, const float *Y
 }
 
 extern "C" size_t gpsig_sig_vjp_workspace_bytes(int n1, int l1, int n2, int l2, int d, int num_levels, int difference) {
+  if (n1 <= 0 || n2 <= 0 || l1 < 1 || l2 < 1 || d <= 0) return 0;
+  if (bwd_wide(d)) return GSC_BYTES + sig_bwd_wide_workspace(n1, l1, n2, l2, d);
   const int DP = bwd_pad(d);
   if (DP == 0 || n1 <= 0 || n2 <= 0 || l1 < 1 || l2 < 1) return 0;
   const BwdGeo geo = bwd_geometry(l2, DP);

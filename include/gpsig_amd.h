@@ -272,6 +272,20 @@ int gpsig_signature_vjp(const float *X, int n, int l, int d, int depth, const fl
 int gpsig_sym_assemble(const float *src, const long long *row_off, long long level_stride, int n, int levels,
                        float *dst, gpsig_stream_t stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * fp32 GEMM on the matrix cores (v_mfma_f32_32x32x2_f32), the engine of the wide-channel paths' inner-
+ * product GEMMs (the PDE increment Gram, the VJPs' emission products).  Exposed for tests:
+ *   C = alpha op(A) op(B) + beta C, row-major, op(A) M x K, op(B) K x N; trans* = 1 transposes.
+ */
+int gpsig_gemm_f32(int transA, int transB, int M, int N, int K, float alpha, const float *A, long long lda,
+                   const float *B, long long ldb, float beta, float *C, long long ldc, gpsig_stream_t stream);
+/* The same with K split into slices whose partial products are summed in a fixed order (products with few
+ * output tiles and a long K); workspace of gpsig_gemm_splitk_bytes(M, N, K) bytes (0: no split). */
+size_t gpsig_gemm_splitk_bytes(int M, int N, int K);
+int gpsig_gemm_f32_splitk(int transA, int transB, int M, int N, int K, float alpha, const float *A, long long lda,
+                          const float *B, long long ldb, float beta, float *C, long long ldc, void *workspace,
+                          size_t workspace_bytes, gpsig_stream_t stream);
+
 /* Library identification (for tests: the loaded object must be this build). */
 const char *gpsig_version(void);
 

@@ -100,3 +100,82 @@ def test_wide_seed_regimes(scale, jumps):
     got = k.K(t(X.reshape(N, -1)), return_levels=True).cpu().numpy()
     exp = kr.SignatureKernelRef(L * D, D, M).K(X.reshape(N, -1), return_levels=True)
     assert (norm_rel_err(got, exp, axis_levels=True) < TOL).all()
+
+
+# ----------------------------------------------------------------------------- gradients
+GTOL = 5e-5
+
+
+@pytest.mark.parametrize("D,L", [(46, 136), (126, 136), (46, 500), (33, 20)])
+@pytest.mark.parametrize("sym", [False, True])
+def test_wide_gram_vjp_raw_levels(D, L, sym):
+    """ops-level VJP of the raw per-level Gram (point-weight tiles + the emission GEMMs) vs fp64 autodiff of
+    the reference graph (oracle/autodiff_ref.py), with and without the forward's saved state."""
+    from gpsig_amd import ops
+    from oracle import autodiff_ref as ar
+    rng = np.random.default_rng(D + L + sym)
+    N1, N2, M = 3, 2, 3
+    X = walks(rng, N1, L, D)
+    Y = None if sym else walks(rng, N2, L - 5, D)
+    n2 = N1 if sym else N2
+    G = rng.standard_normal((M + 1, N1, n2))
+    Xt = torch.tensor(X, device=DEV, dtype=torch.float32)
+    Yt = None if sym else torch.tensor(Y, device=DEV, dtype=torch.float32)
+    Gt = torch.tensor(G, device=DEV, dtype=torch.float32)
+    st = torch.empty(ops.sig_state_numel(N1, None if sym else N2, L if sym else L - 5, M), dtype=torch.float32,
+                     device=DEV)
+    K0 = ops.sig_gram(Xt, Yt, M)
+    K1 = ops.sig_gram(Xt, Yt, M, state=st)
+    assert torch.equal(K0, K1)
+    g0 = ops.sig_gram_vjp(Xt, Yt, M, Gt, gout_levels=True)
+    g1 = ops.sig_gram_vjp(Xt, Yt, M, Gt, gout_levels=True, state=st)
+    Xr = torch.tensor(X, requires_grad=True)
+    Yr = Xr if sym else torch.tensor(Y, requires_grad=True)
+    (ar.k_seq(Xr, Yr, M, "rbf") * torch.tensor(G)).sum().backward()
+    for g in (g0, g1):
+        assert norm_rel_err(g[0].cpu().numpy(), Xr.grad.numpy()) < GTOL
+        if not sym:
+            assert norm_rel_err(g[1].cpu().numpy(), Yr.grad.numpy()) < GTOL
+
+
+@pytest.mark.parametrize("D", [46, 126])
+def test_wide_K_gradient_normalised(D):
+    """K(X, X2) of SignatureRBF (normalised: diagonal VJP chained through rs) with lengthscales and
+    variances, gradients in X, X2, lengthscales, variances vs fp64 autodiff."""
+    import gpsig_amd
+    from oracle import autodiff_ref as ar
+    rng = np.random.default_rng(D + 1)
+    N1, N2, L, M = 4, 3, 30, 4
+    X, X2 = walks(rng, N1, L, D, 2.0), walks(rng, N2, L, D, 2.0)
+    G = rng.standard_normal((N1, N2))
+    ls = rng.uniform(0.7, 1.5, D)
+    var = np.linspace(0.5, 1.5, M + 1)
+    k = gpsig_amd.SignatureRBF(L * D, D, M)
+    k.lengthscales = torch.tensor(ls, device=DEV, requires_grad=True)
+    k.variances = torch.tensor(var, device=DEV, requires_grad=True)
+    Xt = torch.tensor(X.reshape(N1, -1), device=DEV, requires_grad=True)
+    X2t = torch.tensor(X2.reshape(N2, -1), device=DEV, requires_grad=True)
+    (k.K(Xt, X2t) * torch.as_tensor(G, device=DEV)).sum().backward()
+    Xr, X2r = torch.tensor(X, requires_grad=True), torch.tensor(X2, requires_grad=True)
+    lr, vr = torch.tensor(ls, requires_grad=True), torch.tensor(var, requires_grad=True)
+    (ar.K(Xr / lr, X2r / lr, M, scale=vr) * torch.tensor(G)).sum().backward()
+    assert norm_rel_err(Xt.grad.reshape(X.shape).cpu().numpy(), Xr.grad.numpy()) < GTOL
+    assert norm_rel_err(X2t.grad.reshape(X2.shape).cpu().numpy(), X2r.grad.numpy()) < GTOL
+    assert norm_rel_err(k.lengthscales.grad.cpu().numpy(), lr.grad.numpy()) < GTOL
+    assert norm_rel_err(k.variances.grad.cpu().numpy(), vr.grad.numpy()) < GTOL
+
+
+@pytest.mark.parametrize("base,difference", [("linear", True), ("rbf", False), ("linear", False)])
+def test_wide_vjp_other_seeds(base, difference):
+    from gpsig_amd import ops
+    from oracle import autodiff_ref as ar
+    rng = np.random.default_rng(9)
+    D, L, M = 40, 25, 3
+    X, Y = walks(rng, 3, L, D), walks(rng, 2, L + 3, D)
+    G = rng.standard_normal((M + 1, 3, 2))
+    gX, gY = ops.sig_gram_vjp(torch.tensor(X, device=DEV), torch.tensor(Y, device=DEV), M,
+                              torch.tensor(G, device=DEV), base=base, gout_levels=True, difference=difference)
+    Xr, Yr = torch.tensor(X, requires_grad=True), torch.tensor(Y, requires_grad=True)
+    (ar.k_seq(Xr, Yr, M, base, difference=difference) * torch.tensor(G)).sum().backward()
+    assert norm_rel_err(gX.cpu().numpy(), Xr.grad.numpy()) < GTOL
+    assert norm_rel_err(gY.cpu().numpy(), Yr.grad.numpy()) < GTOL
