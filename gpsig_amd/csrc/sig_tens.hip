@@ -72,6 +72,36 @@ GPSIG_DEV float rbf_second_diff(const float (&a)[DP], const float (&da)[DP], con
   return (fast_exp(-0.5f * d11) - fast_exp(-0.5f * d10)) - (fast_exp(-0.5f * d01) - k00);
 }
 
+// The same second difference for a runtime channel count; av/dav/bv/dbv(q) return channel q of a, da, b, db.
+template <class FA, class FDA, class FB, class FDB>
+GPSIG_DEV float rbf_second_diff_rt(int d, FA av, FDA dav, FB bv, FDB dbv) {
+  float diff2 = 0.f, p = 0.f, q = 0.f, c = 0.f, hda = 0.f, hdb = 0.f;
+  float d11 = 0.f, d10 = 0.f, d01 = 0.f;
+  for (int k = 0; k < d; ++k) {
+    const float a = av(k), da = dav(k), b = bv(k), db = dbv(k);
+    const float df = a - b;
+    diff2 = __builtin_fmaf(df, df, diff2);
+    p = __builtin_fmaf(-df, da, p);
+    q = __builtin_fmaf(df, db, q);
+    c = __builtin_fmaf(da, db, c);
+    hda = __builtin_fmaf(da, da, hda);
+    hdb = __builtin_fmaf(db, db, hdb);
+    const float e11 = df + da - db, e10 = df + da, e01 = df - db;
+    d11 = __builtin_fmaf(e11, e11, d11);
+    d10 = __builtin_fmaf(e10, e10, d10);
+    d01 = __builtin_fmaf(e01, e01, d01);
+  }
+  p -= 0.5f * hda;
+  q -= 0.5f * hdb;
+  const float k00 = fast_exp(-0.5f * diff2);
+  const float mx = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(p), __builtin_fabsf(q)), __builtin_fabsf(c));
+  if (mx < EM1_TAU) {
+    const float Ep = em1_small(p), Eq = em1_small(q), Ec = em1_small(c);
+    return k00 * __builtin_fmaf(Ep, Eq, (1.0f + Ep) * (1.0f + Eq) * Ec);
+  }
+  return (fast_exp(-0.5f * d11) - fast_exp(-0.5f * d10)) - (fast_exp(-0.5f * d01) - k00);
+}
+
 // ------------------------------------------------------------------------------------ tens vs seq
 struct TvsArgs {
   const float *Z;  // (LT, T, [2,] d)
@@ -152,8 +182,60 @@ GPSIG_DEV float tvs_seed(const TvsArgs &a, const float *zs, int k, const TvsCell
   return rbf_second_diff<DP>(z0, dz, cl.x, cl.dx);
 }
 
+// tvs_seed for a runtime channel count (DP == 0 instantiation): the cell's channels are read from the
+// time-major features, channel q of x_pt at fr[q n], of x_{pt+1} at fn[q n], of dx_pt at fr[(d + q) n].
+GPSIG_DEV float tvs_seed_wide(const TvsArgs &a, const float *zs, int k, const float *fr, const float *fn, float beta,
+                              float &kc) {
+  const int d = a.d;
+  const long long n = a.n;
+  const float *zt = zs + k * (a.incr ? 2 * d : d);
+  auto xq = [&](int q) { return fr[q * n]; };
+  auto dxq = [&](int q) { return fr[(d + q) * n]; };
+  if (!a.rbf) {
+    float v = 0.f;
+    for (int q = 0; q < d; ++q) {
+      const float zq = a.incr ? zt[d + q] - zt[q] : zt[q];
+      v = __builtin_fmaf(zq, a.diff ? dxq(q) : xq(q), v);
+    }
+    return v;
+  }
+  if (!a.incr) {
+    if (!a.diff) {
+      float s2 = 0.f;
+      for (int q = 0; q < d; ++q) {
+        const float df = zt[q] - xq(q);
+        s2 = __builtin_fmaf(df, df, s2);
+      }
+      return fast_exp(-0.5f * s2);
+    }
+    float s2 = 0.f, zdx = 0.f;
+    for (int q = 0; q < d; ++q) {
+      const float df = zt[q] - fn[q * n];
+      s2 = __builtin_fmaf(df, df, s2);
+      zdx = __builtin_fmaf(zt[q], dxq(q), zdx);
+    }
+    const float kn = fast_exp(-0.5f * s2);
+    const float qv = zdx - beta;
+    const float kcur = kc;
+    kc = kn;
+    return __builtin_fabsf(qv) < EM1_TAU ? kcur * em1_small(qv) : kn - kcur;
+  }
+  if (!a.diff) {
+    float s0 = 0.f, s1 = 0.f;
+    for (int q = 0; q < d; ++q) {
+      const float e0 = zt[q] - xq(q), e1 = zt[d + q] - xq(q);
+      s0 = __builtin_fmaf(e0, e0, s0);
+      s1 = __builtin_fmaf(e1, e1, s1);
+    }
+    return fast_exp(-0.5f * s1) - fast_exp(-0.5f * s0);
+  }
+  return rbf_second_diff_rt(
+      d, [&](int q) { return zt[q]; }, [&](int q) { return zt[d + q] - zt[q]; }, xq, dxq);
+}
+
 // One wave per block; the per-(level, stage) running sums and the carried k values live in this
 // lane's LDS column (dynamic indices, no register arrays), the levels' stage chains are plain loops.
+// DP == 0: any channel count (tvs_seed_wide reads the cell's channels from the features per component).
 template <int DP>
 __global__ __launch_bounds__(64) void tvs_kernel(TvsArgs a) {
   extern __shared__ __attribute__((aligned(16))) float lds[];
@@ -193,27 +275,35 @@ __global__ __launch_bounds__(64) void tvs_kernel(TvsArgs a) {
   }
   const int npts = a.diff ? a.l - 1 : a.l;
   for (int pt = 0; pt < npts; ++pt) {
-    TvsCell<DP> cl;
+    TvsCell<DP == 0 ? 1 : DP> cl;
     const float *fr = a.Ft + (long long)pt * FC * n + s;
     const float *fn = fr + (long long)FC * n;
+    if constexpr (DP > 0) {
 #pragma unroll
-    for (int q = 0; q < DP; ++q) {
-      cl.x[q] = q < d ? fr[(long long)q * n] : 0.f;
-      cl.dx[q] = q < d ? fr[(long long)(d + q) * n] : 0.f;
-      cl.xn[q] = (carry && q < d) ? fn[(long long)q * n] : 0.f;
+      for (int q = 0; q < DP; ++q) {
+        cl.x[q] = q < d ? fr[(long long)q * n] : 0.f;
+        cl.dx[q] = q < d ? fr[(long long)(d + q) * n] : 0.f;
+        cl.xn[q] = (carry && q < d) ? fn[(long long)q * n] : 0.f;
+      }
     }
     cl.beta = fr[(long long)(2 * d + 1) * n];
+    auto seed = [&](int k, float &kk) -> float {
+      if constexpr (DP == 0)
+        return tvs_seed_wide(a, zl, k, fr, fn, cl.beta, kk);
+      else
+        return tvs_seed<DP>(a, zl, k, cl, kk);
+    };
     // level i uses components k0 .. k0+i-1 (k0 = i(i-1)/2); stage st runs on component k0+st
     for (int i = 1; i <= M; ++i) {
       const int k0 = i * (i - 1) / 2;
       float kk = kc[k0 * 64];
-      const float m0 = tvs_seed<DP>(a, zl, k0, cl, kk);
+      const float m0 = seed(k0, kk);
       kc[k0 * 64] = kk;
       if (a.order <= 1) {
         float prev = m0;  // R_0(pt)
         for (int st = 1; st < i; ++st) {
           float kq = kc[(k0 + st) * 64];
-          const float mk = tvs_seed<DP>(a, zl, k0 + st, cl, kq);
+          const float mk = seed(k0 + st, kq);
           kc[(k0 + st) * 64] = kq;
           const float ss = Ssum[(k0 + st - 1) * 64];
           Ssum[(k0 + st - 1) * 64] = ss + prev;
@@ -232,7 +322,7 @@ __global__ __launch_bounds__(64) void tvs_kernel(TvsArgs a) {
 #pragma unroll
           for (int b = 0; b < TV_MMAX; ++b) tot += blk[b];
           float kq = kc[(k0 + st) * 64];
-          const float mk = tvs_seed<DP>(a, zl, k0 + st, cl, kq);
+          const float mk = seed(k0 + st, kq);
           kc[(k0 + st) * 64] = kq;
 #pragma unroll
           for (int b = TV_MMAX - 1; b >= 1; --b) blk[b] = (b < dn) ? mk * blk[b - 1] / (float)(b + 1) : 0.f;
@@ -287,6 +377,16 @@ __global__ __launch_bounds__(256) void tens_gram_kernel(TgArgs a) {
       } else {
         // kernels.py:278  M[1,1] + M[0,0] - M[1,0] - M[0,1]
         const float *za = a.Z + (((long long)k * a.t + t1) * 2) * d, *zb = a.Z + (((long long)k * a.t + t2) * 2) * d;
+        if constexpr (DP == 0) {  // any channel count
+          if (a.rbf) {
+            v = rbf_second_diff_rt(
+                d, [&](int q) { return za[q]; }, [&](int q) { return za[d + q] - za[q]; }, [&](int q) { return zb[q]; },
+                [&](int q) { return zb[d + q] - zb[q]; });
+          } else {
+            v = 0.f;
+            for (int q = 0; q < d; ++q) v = __builtin_fmaf(za[d + q] - za[q], zb[d + q] - zb[q], v);
+          }
+        } else {
         float A0[DP], dA[DP], B0[DP], dB[DP];
 #pragma unroll
         for (int q = 0; q < DP; ++q) {
@@ -300,6 +400,7 @@ __global__ __launch_bounds__(256) void tens_gram_kernel(TgArgs a) {
         } else {
           v = 0.f;
           for (int q = 0; q < d; ++q) v = __builtin_fmaf(dA[q], dB[q], v);
+        }
         }
       }
       prod = (st == 0) ? v : v * prod;
@@ -331,30 +432,41 @@ __global__ __launch_bounds__(64) void rescaled_kernel(RsArgs a) {
   const int d = a.d, L = a.l;
   const float *x = a.X + (long long)nn * L * d;
   constexpr int LT = M * (M + 1) / 2;
+  // DP == 0: any channel count; every stage seed of a row comes from one runtime channel loop (sd below)
+  constexpr bool WIDE = DP == 0;
+  constexpr int DPA = WIDE ? 1 : DP;
   // lambda of component r for this tensor (wave-uniform), staged in LDS once (the compiler would
   // otherwise emit serialised vector loads for it inside the row loop); the ones tensor of the
   // concatenation (kernels.py:812) is tt == T
-  __shared__ float lz[LT * DP];
-  for (int e = lane; e < LT * DP; e += 64) {
-    const int r = e / DP, q = e % DP;
-    lz[e] = (q < d) ? ((tt < a.t) ? a.Z[((long long)r * a.t + tt) * d + q] : 1.0f) : 0.f;
+  __shared__ float lz[LT * DPA];
+  if constexpr (!WIDE) {
+    for (int e = lane; e < LT * DP; e += 64) {
+      const int r = e / DP, q = e % DP;
+      lz[e] = (q < d) ? ((tt < a.t) ? a.Z[((long long)r * a.t + tt) * d + q] : 1.0f) : 0.f;
+    }
+    __syncthreads();
   }
-  __syncthreads();
-  auto lam = [&](int r, int q) -> float { return lz[r * DP + q]; };
+  auto lam = [&](int r, int q) -> float { return lz[r * DPA + q]; };
   // this lane's columns q0 = lane*W + w
-  float xc[W][DP], dxc[W][DP];
+  float xc[W][DPA], dxc[W][DPA];
   bool valid[W];
+  int jjw[W];
 #pragma unroll
   for (int w = 0; w < W; ++w) {
     const int j = lane * W + w;
     valid[w] = j < L - 1;
     const int jj = j < L - 1 ? j : L - 2;
+    jjw[w] = jj;
+    if constexpr (!WIDE) {
 #pragma unroll
-    for (int q = 0; q < DP; ++q) {
-      xc[w][q] = q < d ? x[jj * d + q] : 0.f;
-      dxc[w][q] = q < d ? x[(jj + 1) * d + q] - x[jj * d + q] : 0.f;
+      for (int q = 0; q < DP; ++q) {
+        xc[w][q] = q < d ? x[jj * d + q] : 0.f;
+        dxc[w][q] = q < d ? x[(jj + 1) * d + q] - x[jj * d + q] : 0.f;
+      }
     }
   }
+  cfloat *xcst = as_const(x);
+  cfloat *zcst = as_const(a.Z);
   // CB[level i][stage s][b]: column running sums over previous rows of sum_a R[s][a][b]
   constexpr int NCB = M * (M + 1) * (M + 2) / 6;  // sum_i sum_{s<i} (s+1)
   float CB[NCB][W];
@@ -367,14 +479,42 @@ __global__ __launch_bounds__(64) void rescaled_kernel(RsArgs a) {
   for (int i = 0; i <= M; ++i) K[i] = 0.f;
 
   for (int pr = 0; pr < L - 1; ++pr) {
-    float xr[DP], dxr[DP];
+    float xr[DPA], dxr[DPA];
+    // per-coordinate increments delta_d(pr, col)
+    float del[W][DPA];
+    // WIDE: every component's stage seed of this row, sd[r][w] = sum_q lam_{r,q} delta_q(pr, col w)
+    float sd[WIDE ? LT : 1][W];
+    if constexpr (WIDE) {
+#pragma unroll
+      for (int r = 0; r < LT; ++r)
+#pragma unroll
+        for (int w = 0; w < W; ++w) sd[r][w] = 0.f;
+      for (int q = 0; q < d; ++q) {
+        const float xq = xcst[pr * d + q], dxq = xcst[(pr + 1) * d + q] - xq;
+        float dl[W];
+#pragma unroll
+        for (int w = 0; w < W; ++w) {
+          const float xw = x[jjw[w] * d + q], dxw = x[(jjw[w] + 1) * d + q] - xw;
+          if (a.emb == 0) {
+            dl[w] = dxq * dxw;
+          } else {
+            const float av[1] = {xq}, dav[1] = {dxq}, bv[1] = {xw}, dbv[1] = {dxw};
+            dl[w] = rbf_second_diff<1>(av, dav, bv, dbv);
+          }
+        }
+#pragma unroll
+        for (int r = 0; r < LT; ++r) {
+          const float lq = tt < a.t ? zcst[((long long)r * a.t + tt) * d + q] : 1.0f;
+#pragma unroll
+          for (int w = 0; w < W; ++w) sd[r][w] = __builtin_fmaf(lq, dl[w], sd[r][w]);
+        }
+      }
+    } else {
 #pragma unroll
     for (int q = 0; q < DP; ++q) {
       xr[q] = q < d ? x[pr * d + q] : 0.f;
       dxr[q] = q < d ? x[(pr + 1) * d + q] - x[pr * d + q] : 0.f;
     }
-    // per-coordinate increments delta_d(pr, col)
-    float del[W][DP];
 #pragma unroll
     for (int w = 0; w < W; ++w)
 #pragma unroll
@@ -386,6 +526,18 @@ __global__ __launch_bounds__(64) void rescaled_kernel(RsArgs a) {
           del[w][q] = (q < d) ? rbf_second_diff<1>(av, dav, bv, dbv) : 0.f;
         }
       }
+    }
+    // stage seed of component r for column w
+    auto seedv = [&](int r, int w) -> float {
+      if constexpr (WIDE) {
+        return sd[r][w];
+      } else {
+        float sv = 0.f;
+#pragma unroll
+        for (int q = 0; q < DP; ++q) sv = __builtin_fmaf(lam(r, q), del[w][q], sv);
+        return sv;
+      }
+    };
     int cbo = 0;
 #pragma unroll
     for (int i = 1; i <= M; ++i) {
@@ -399,12 +551,7 @@ __global__ __launch_bounds__(64) void rescaled_kernel(RsArgs a) {
 #pragma unroll
           for (int w = 0; w < W; ++w) R[x1][y1][w] = 0.f;
 #pragma unroll
-      for (int w = 0; w < W; ++w) {
-        float sv = 0.f;
-#pragma unroll
-        for (int q = 0; q < DP; ++q) sv = __builtin_fmaf(lam(r0, q), del[w][q], sv);
-        R[0][0][w] = valid[w] ? sv : 0.f;
-      }
+      for (int w = 0; w < W; ++w) R[0][0][w] = valid[w] ? seedv(r0, w) : 0.f;
 #pragma unroll
       for (int st = 0; st < i; ++st) {
         const int dm = st + 1;  // blocks of stage st (full order: num_levels >= i)
@@ -426,12 +573,7 @@ __global__ __launch_bounds__(64) void rescaled_kernel(RsArgs a) {
           const int dn = st + 2;
           float seed[W];
 #pragma unroll
-          for (int w = 0; w < W; ++w) {
-            float sv = 0.f;
-#pragma unroll
-            for (int q = 0; q < DP; ++q) sv = __builtin_fmaf(lam(r0 + st + 1, q), del[w][q], sv);
-            seed[w] = valid[w] ? sv : 0.f;
-          }
+          for (int w = 0; w < W; ++w) seed[w] = valid[w] ? seedv(r0 + st + 1, w) : 0.f;
           float tot[W], S00[W];
 #pragma unroll
           for (int w = 0; w < W; ++w) {
@@ -527,11 +669,14 @@ __global__ void rescaled_combine_kernel(float *out, const float *kones, int M, i
 
 using namespace gpsig;
 
+// channel padding of the fixed instantiations; 0 = the runtime-channel (wide) instantiation
 static int dpad4(int d) { return d <= 4 ? 4 : d <= 8 ? 8 : d <= 16 ? 16 : d <= 32 ? 32 : 0; }
 
 namespace gpsig {
 int tvs_pk_launch(const float *Z, int lt, int t, int increments, int d, const float *Ft, int n, int l, int M,
                   float *out, float *Zp, bool rbf, float *state, hipStream_t s);
+int tvs_wide_launch(const float *Z, int lt, int t, int increments, int d, const float *Ft, int n, int l, int M,
+                    float *out, float *Zw, bool rbf, float *state, hipStream_t s);
 size_t tvs_pk_zp_bytes(int lt, int t, int d);
 }  // namespace gpsig
 
@@ -562,26 +707,31 @@ extern "C" int gpsig_tens_vs_seq(const float *Z, int lt, int t, int increments, 
   if (num_levels > TV_MMAX || order < 1 || t > 65535) return GPSIG_EUNSUPPORTED;
   if (base_kind != GPSIG_BASE_RBF && base_kind != GPSIG_BASE_LINEAR) return GPSIG_EUNSUPPORTED;
   const int DP = dpad4(d);
-  if (DP == 0) return GPSIG_EUNSUPPORTED;
   if (!workspace || workspace_bytes < gpsig_tens_workspace_bytes(n, l, d, lt, t)) return GPSIG_EWORKSPACE;
   float *Ft = static_cast<float *>(workspace);
   const long long tot = (long long)n * l;
   hipLaunchKernelGGL(tvs_features_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, X, n, l, d, Ft);
   if (difference && order == 1) {
-    // packed fast paths: RBF (exp-free recurrences) and linear
+    // packed fast paths: RBF (exp-free recurrences) and linear, d <= 8; any channel count: the same
+    // recursion with a runtime channel loop
     float *Zp = reinterpret_cast<float *>(static_cast<char *>(workspace) + tvs_ft_bytes(n, l, d));
-    const int rc = tvs_pk_launch(Z, lt, t, increments, d, Ft, n, l, num_levels, out, Zp,
-                                 base_kind == GPSIG_BASE_RBF, nullptr, s);
+    int rc = tvs_pk_launch(Z, lt, t, increments, d, Ft, n, l, num_levels, out, Zp, base_kind == GPSIG_BASE_RBF,
+                           nullptr, s);
+    if (rc == -1 && d > 8)
+      rc = tvs_wide_launch(Z, lt, t, increments, d, Ft, n, l, num_levels, out, Zp, base_kind == GPSIG_BASE_RBF,
+                           nullptr, s);
     if (rc != -1) return rc;
   }
   TvsArgs a{Z, Ft, lt, t, n, l, d, num_levels, order, increments, difference, base_kind == GPSIG_BASE_RBF, out};
   dim3 grid((n + 63) / 64, t);
   const size_t lds = ((size_t)2 * 64 * lt + (size_t)lt * (increments ? 2 : 1) * d) * sizeof(float);
+  if (lds > 160 * 1024) return GPSIG_EUNSUPPORTED;
   switch (DP) {
     case 4: hipLaunchKernelGGL(tvs_kernel<4>, grid, dim3(64), lds, s, a); break;
     case 8: hipLaunchKernelGGL(tvs_kernel<8>, grid, dim3(64), lds, s, a); break;
     case 16: hipLaunchKernelGGL(tvs_kernel<16>, grid, dim3(64), lds, s, a); break;
-    default: hipLaunchKernelGGL(tvs_kernel<32>, grid, dim3(64), lds, s, a); break;
+    case 32: hipLaunchKernelGGL(tvs_kernel<32>, grid, dim3(64), lds, s, a); break;
+    default: hipLaunchKernelGGL(tvs_kernel<0>, grid, dim3(64), lds, s, a); break;
   }
   return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
 }
@@ -597,14 +747,16 @@ extern "C" int gpsig_tens_vs_seq_state(const float *Z, int lt, int t, int increm
     return GPSIG_EINVAL;
   if (lt != num_levels * (num_levels + 1) / 2) return GPSIG_EINVAL;
   if (base_kind != GPSIG_BASE_RBF && base_kind != GPSIG_BASE_LINEAR) return GPSIG_EUNSUPPORTED;
-  if (num_levels > 6 || d > 8 || t > 65535) return GPSIG_EUNSUPPORTED;
+  if (num_levels > TV_MMAX || t > 65535) return GPSIG_EUNSUPPORTED;
+  if (d <= 8 && num_levels > 6) return GPSIG_EUNSUPPORTED;  // the packed paths' levels
   if (!workspace || workspace_bytes < gpsig_tens_workspace_bytes(n, l, d, lt, t)) return GPSIG_EWORKSPACE;
   float *Ft = static_cast<float *>(workspace);
   const long long tot = (long long)n * l;
   hipLaunchKernelGGL(tvs_features_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, X, n, l, d, Ft);
   float *Zp = reinterpret_cast<float *>(static_cast<char *>(workspace) + tvs_ft_bytes(n, l, d));
-  const int rc = tvs_pk_launch(Z, lt, t, increments, d, Ft, n, l, num_levels, out, Zp, base_kind == GPSIG_BASE_RBF,
-                               state, s);
+  int rc = tvs_pk_launch(Z, lt, t, increments, d, Ft, n, l, num_levels, out, Zp, base_kind == GPSIG_BASE_RBF, state, s);
+  if (rc == -1 && d > 8)
+    rc = tvs_wide_launch(Z, lt, t, increments, d, Ft, n, l, num_levels, out, Zp, base_kind == GPSIG_BASE_RBF, state, s);
   return rc == -1 ? GPSIG_EUNSUPPORTED : rc;
 }
 
@@ -616,14 +768,14 @@ extern "C" int gpsig_tens_gram(const float *Z, int lt, int t, int increments, in
   if (num_levels > TV_MMAX) return GPSIG_EUNSUPPORTED;
   if (base_kind != GPSIG_BASE_RBF && base_kind != GPSIG_BASE_LINEAR) return GPSIG_EUNSUPPORTED;
   const int DP = dpad4(d);
-  if (DP == 0) return GPSIG_EUNSUPPORTED;
   TgArgs a{Z, lt, t, d, num_levels, increments, base_kind == GPSIG_BASE_RBF, out};
   dim3 grid((t + 255) / 256, t);
   switch (DP) {
     case 4: hipLaunchKernelGGL(tens_gram_kernel<4>, grid, dim3(256), 0, s, a); break;
     case 8: hipLaunchKernelGGL(tens_gram_kernel<8>, grid, dim3(256), 0, s, a); break;
     case 16: hipLaunchKernelGGL(tens_gram_kernel<16>, grid, dim3(256), 0, s, a); break;
-    default: hipLaunchKernelGGL(tens_gram_kernel<32>, grid, dim3(256), 0, s, a); break;
+    case 32: hipLaunchKernelGGL(tens_gram_kernel<32>, grid, dim3(256), 0, s, a); break;
+    default: hipLaunchKernelGGL(tens_gram_kernel<0>, grid, dim3(256), 0, s, a); break;
   }
   return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
 }
@@ -638,18 +790,24 @@ struct TgBwdArgs {
   int t, d, incr, rbf, chunk;
   const float *gout;  // (M+1, T, T)
   float *gZ;          // like Z, accumulated
+  int q0;             // WIDE: this launch accumulates the channels q0 .. q0 + DP - 1 of the gradient
 };
 
-template <int DP>
+// WIDE: the component values m_c are products over all d channels (runtime loops), the gradient
+// accumulators cover one window of DP channels (the host launches one window after the other).
+template <int DP, bool WIDE = false>
 __global__ __launch_bounds__(64) void tens_gram_vjp_kernel(TgBwdArgs a) {
   const int t1 = blockIdx.x * 64 + threadIdx.x;
   if (t1 >= a.t) return;
   const int i = blockIdx.y + 1, k0 = i * (i - 1) / 2;
   const int tb = blockIdx.z * a.chunk, te = min(a.t, tb + a.chunk);
   const int d = a.d, T = a.t, zs = a.incr ? 2 * d : d;
+  const int q0 = WIDE ? a.q0 : 0;
   auto zv = [&](int k, int tt, int h, int q) -> float {
     return q < d ? a.Z[((long long)k * T + tt) * zs + h * d + q] : 0.f;
   };
+  // the accumulated window: channel q0 + q
+  auto zw = [&](int k, int tt, int h, int q) -> float { return zv(k, tt, h, q0 + q); };
   float g0[TV_MMAX][DP], g1[TV_MMAX][DP];
 #pragma unroll
   for (int c = 0; c < TV_MMAX; ++c)
@@ -662,7 +820,25 @@ __global__ __launch_bounds__(64) void tens_gram_vjp_kernel(TgBwdArgs a) {
     for (int c = 0; c < TV_MMAX; ++c) {
       if (c >= i) break;
       const int k = k0 + c;
-      if (!a.incr) {
+      if constexpr (WIDE) {
+        if (!a.incr) {
+          float s2 = 0.f, ip = 0.f;
+          for (int q = 0; q < d; ++q) {
+            const float df = zv(k, t1, 0, q) - zv(k, t2, 0, q);
+            s2 = __builtin_fmaf(df, df, s2);
+            ip = __builtin_fmaf(zv(k, t1, 0, q), zv(k, t2, 0, q), ip);
+          }
+          m[c] = a.rbf ? fast_exp(-0.5f * s2) : ip;
+        } else if (a.rbf) {
+          m[c] = rbf_second_diff_rt(
+              d, [&](int q) { return zv(k, t1, 0, q); }, [&](int q) { return zv(k, t1, 1, q) - zv(k, t1, 0, q); },
+              [&](int q) { return zv(k, t2, 0, q); }, [&](int q) { return zv(k, t2, 1, q) - zv(k, t2, 0, q); });
+        } else {
+          float v = 0.f;
+          for (int q = 0; q < d; ++q) v = __builtin_fmaf(zv(k, t1, 1, q) - zv(k, t1, 0, q), zv(k, t2, 1, q) - zv(k, t2, 0, q), v);
+          m[c] = v;
+        }
+      } else if (!a.incr) {
         float s2 = 0.f, ip = 0.f;
 #pragma unroll
         for (int q = 0; q < DP; ++q) {
@@ -701,26 +877,27 @@ __global__ __launch_bounds__(64) void tens_gram_vjp_kernel(TgBwdArgs a) {
       const float w = Gs * pre[c] * suf;
       suf *= m[c];
       const int k = k0 + c;
+      const int nq = WIDE ? d : DP;  // channels of the distances (all of them)
       if (!a.incr) {
         if (a.rbf) {
           float s2 = 0.f;
-#pragma unroll
-          for (int q = 0; q < DP; ++q) {
+
+          for (int q = 0; q < nq; ++q) {
             const float df = zv(k, t2, 0, q) - zv(k, t1, 0, q);
             s2 = __builtin_fmaf(df, df, s2);
           }
           const float wk = w * fast_exp(-0.5f * s2);
 #pragma unroll
-          for (int q = 0; q < DP; ++q) g0[c][q] = __builtin_fmaf(wk, zv(k, t2, 0, q) - zv(k, t1, 0, q), g0[c][q]);
+          for (int q = 0; q < DP; ++q) g0[c][q] = __builtin_fmaf(wk, zw(k, t2, 0, q) - zw(k, t1, 0, q), g0[c][q]);
         } else {
 #pragma unroll
-          for (int q = 0; q < DP; ++q) g0[c][q] = __builtin_fmaf(w, zv(k, t2, 0, q), g0[c][q]);
+          for (int q = 0; q < DP; ++q) g0[c][q] = __builtin_fmaf(w, zw(k, t2, 0, q), g0[c][q]);
         }
       } else if (a.rbf) {
         // dM/dA1 = k(A1,B1)(B1 - A1) - k(A1,B0)(B0 - A1),  dM/dA0 = k(A0,B0)(B0 - A0) - k(A0,B1)(B1 - A0)
         float e11 = 0.f, e10 = 0.f, e00 = 0.f, e01 = 0.f;
-#pragma unroll
-        for (int q = 0; q < DP; ++q) {
+
+        for (int q = 0; q < nq; ++q) {
           const float a0 = zv(k, t1, 0, q), a1 = zv(k, t1, 1, q), b0 = zv(k, t2, 0, q), b1 = zv(k, t2, 1, q);
           e11 = __builtin_fmaf(a1 - b1, a1 - b1, e11);
           e10 = __builtin_fmaf(a1 - b0, a1 - b0, e10);
@@ -731,14 +908,14 @@ __global__ __launch_bounds__(64) void tens_gram_vjp_kernel(TgBwdArgs a) {
         const float k00 = w * fast_exp(-0.5f * e00), k01 = w * fast_exp(-0.5f * e01);
 #pragma unroll
         for (int q = 0; q < DP; ++q) {
-          const float a0 = zv(k, t1, 0, q), a1 = zv(k, t1, 1, q), b0 = zv(k, t2, 0, q), b1 = zv(k, t2, 1, q);
+          const float a0 = zw(k, t1, 0, q), a1 = zw(k, t1, 1, q), b0 = zw(k, t2, 0, q), b1 = zw(k, t2, 1, q);
           g1[c][q] += k11 * (b1 - a1) - k10 * (b0 - a1);
           g0[c][q] += k00 * (b0 - a0) - k01 * (b1 - a0);
         }
       } else {
 #pragma unroll
         for (int q = 0; q < DP; ++q) {
-          const float dBq = zv(k, t2, 1, q) - zv(k, t2, 0, q);
+          const float dBq = zw(k, t2, 1, q) - zw(k, t2, 0, q);
           g1[c][q] = __builtin_fmaf(w, dBq, g1[c][q]);
           g0[c][q] = __builtin_fmaf(-w, dBq, g0[c][q]);
         }
@@ -748,10 +925,13 @@ __global__ __launch_bounds__(64) void tens_gram_vjp_kernel(TgBwdArgs a) {
 #pragma unroll
   for (int c = 0; c < TV_MMAX; ++c) {
     if (c >= i) break;
-    float *gz = a.gZ + ((long long)(k0 + c) * T + t1) * zs;
-    for (int q = 0; q < d; ++q) {
-      unsafeAtomicAdd(gz + q, g0[c][q]);
-      if (a.incr) unsafeAtomicAdd(gz + d + q, g1[c][q]);
+    float *gz = a.gZ + ((long long)(k0 + c) * T + t1) * zs + q0;
+#pragma unroll
+    for (int q = 0; q < DP; ++q) {
+      if (q0 + q < d) {
+        unsafeAtomicAdd(gz + q, g0[c][q]);
+        if (a.incr) unsafeAtomicAdd(gz + d + q, g1[c][q]);
+      }
     }
   }
 }
@@ -762,6 +942,7 @@ static int launch_rs(const RsArgs &a, int DP, hipStream_t s) {
   switch (DP) {
     case 4: hipLaunchKernelGGL((rescaled_kernel<M, W, 4>), grid, dim3(64), 0, s, a); break;
     case 8: hipLaunchKernelGGL((rescaled_kernel<M, W, 8>), grid, dim3(64), 0, s, a); break;
+    case 0: hipLaunchKernelGGL((rescaled_kernel<M, W, 0>), grid, dim3(64), 0, s, a); break;
     default: return GPSIG_EUNSUPPORTED;
   }
   return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
@@ -787,8 +968,7 @@ extern "C" int gpsig_rescaled(const float *Z, int lt, int t, const float *X, int
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (!Z || !X || !out || t <= 0 || n <= 0 || l < 2 || d <= 0 || num_levels < 1) return GPSIG_EINVAL;
   if (lt != num_levels * (num_levels + 1) / 2 || (embedding != 0 && embedding != 1)) return GPSIG_EINVAL;
-  const int DP = dpad4(d);
-  if (DP == 0 || DP > 8) return GPSIG_EUNSUPPORTED;
+  const int DP = d <= 8 ? dpad4(d) : 0;  // 0: runtime channel loop
   if (!workspace || workspace_bytes < gpsig_rescaled_workspace_bytes(n, num_levels)) return GPSIG_EWORKSPACE;
   RsArgs a{Z, X, lt, t, n, l, d, num_levels, embedding, out, static_cast<float *>(workspace)};
   int rc;
@@ -816,15 +996,20 @@ extern "C" int gpsig_tens_gram_vjp(const float *Z, int lt, int t, int increments
   if (num_levels > TV_MMAX) return GPSIG_EUNSUPPORTED;
   if (base_kind != GPSIG_BASE_RBF && base_kind != GPSIG_BASE_LINEAR) return GPSIG_EUNSUPPORTED;
   const int DP = dpad4(d);
-  if (DP == 0) return GPSIG_EUNSUPPORTED;
   const int chunk = 64;
-  TgBwdArgs a{Z, t, d, increments, base_kind == GPSIG_BASE_RBF, chunk, gout, gZ};
+  TgBwdArgs a{Z, t, d, increments, base_kind == GPSIG_BASE_RBF, chunk, gout, gZ, 0};
   dim3 grid((t + 63) / 64, num_levels, (t + chunk - 1) / chunk);
   switch (DP) {
     case 4: hipLaunchKernelGGL(tens_gram_vjp_kernel<4>, grid, dim3(64), 0, s, a); break;
     case 8: hipLaunchKernelGGL(tens_gram_vjp_kernel<8>, grid, dim3(64), 0, s, a); break;
     case 16: hipLaunchKernelGGL(tens_gram_vjp_kernel<16>, grid, dim3(64), 0, s, a); break;
-    default: hipLaunchKernelGGL(tens_gram_vjp_kernel<32>, grid, dim3(64), 0, s, a); break;
+    case 32: hipLaunchKernelGGL(tens_gram_vjp_kernel<32>, grid, dim3(64), 0, s, a); break;
+    default:  // wide: windows of 16 gradient channels, the component products over all d
+      for (int q0 = 0; q0 < d; q0 += 16) {
+        a.q0 = q0;
+        hipLaunchKernelGGL((tens_gram_vjp_kernel<16, true>), grid, dim3(64), 0, s, a);
+      }
+      break;
   }
   return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
 }

@@ -8,6 +8,10 @@ size_t tvs_features_bytes(int n, int l, int d);
 int tvs_features_launch(const float *X, int n, int l, int d, float *Ft, hipStream_t s);
 template <int DP, bool INCR>
 int tvs_bwd_launch_dp(const TvsBwdArgs &a, int M, bool rbf, bool diff, hipStream_t s);
+size_t tvs_bwd_wide_workspace(int n, int l, int d, int lt, int t);
+int tvs_bwd_wide(const float *Z, int lt, int t, int incr, int d, const float *X, int n, int l, int M, bool rbf,
+                 bool diff, const float *gout, float *gZ, float *gX, const float *state, void *workspace,
+                 size_t workspace_bytes, hipStream_t s);
 
 // gX[seq][s][q] += gXt[(s * d + q) * n + seq]
 __global__ __launch_bounds__(256) void tvs_gx_add_kernel(const float *__restrict__ gXt, int n, int l, int d,
@@ -30,6 +34,12 @@ extern "C" size_t gpsig_tens_vjp_workspace_bytes(int n, int l, int d) {
   return tvs_features_bytes(n, l, d) + align256((size_t)n * l * d * sizeof(float));
 }
 
+// Channel counts past the instantiations (d > 16): point-weight tiles + GEMMs (sig_tvs_bwd_wide.hip); the
+// workspace depends on the tensors too
+extern "C" size_t gpsig_tens_vjp_wide_workspace_bytes(int n, int l, int d, int lt, int t) {
+  return tvs_bwd_wide_workspace(n, l, d, lt, t);
+}
+
 extern "C" int gpsig_tens_vs_seq_vjp(const float *Z, int lt, int t, int increments, int d, const float *X, int n,
                                      int l, int num_levels, int base_kind, int difference, const float *gout,
                                      float *gZ, float *gX, const float *state,
@@ -42,7 +52,10 @@ extern "C" int gpsig_tens_vs_seq_vjp(const float *Z, int lt, int t, int incremen
   if (state && !difference) return GPSIG_EINVAL;  // the saved state comes from the difference fast paths
   if (base_kind != GPSIG_BASE_RBF && base_kind != GPSIG_BASE_LINEAR) return GPSIG_EUNSUPPORTED;
   const int DP = tvs_bwd_pad(d);
-  if (DP == 0 || num_levels > 8 || t > 65535) return GPSIG_EUNSUPPORTED;
+  if (num_levels > 8 || t > 65535) return GPSIG_EUNSUPPORTED;
+  if (DP == 0)
+    return tvs_bwd_wide(Z, lt, t, increments, d, X, n, l, num_levels, base_kind == GPSIG_BASE_RBF, difference != 0, gout,
+                        gZ, gX, state, workspace, workspace_bytes, s);
   if (!workspace || workspace_bytes < gpsig_tens_vjp_workspace_bytes(n, l, d)) return GPSIG_EWORKSPACE;
   float *Ft = static_cast<float *>(workspace);
   float *gXt = reinterpret_cast<float *>(static_cast<char *>(workspace) + tvs_features_bytes(n, l, d));

@@ -315,6 +315,241 @@ __global__ __launch_bounds__(64) void tvs_lin_kernel(TvsPkArgs a) {
   }
 }
 
+// ------------------------------------------------------------------------------------ wide channels
+// The same recursion and seeds (tvs_pk_kernel, tvs_lin_kernel) for any channel count: the per-step dots
+// <z_k, dx_s> (and <dz_k, dx_s>) of all LT components come from one runtime channel loop -- the lane's
+// dx_s[q] is loaded once per channel (coalesced, time-major features) and the wave-uniform component
+// values of that channel are scalar loads from the prepared [tensor][channel][component] buffer, so
+// nothing grows with d except the loop count.  One sequence per lane.
+struct TvsWideArgs {
+  const float *Zw;  // (T, [2,] d, LT) then (T, LT) |dz|^2 / 2: tvs_wide_prep_kernel
+  const float *Ft;  // time-major features (sig_tens.hip)
+  int t, n, l, d;
+  float *out;
+  float *state;
+};
+
+__host__ __device__ inline long long tvs_wide_zs(int d, int lt, bool incr) { return (long long)(incr ? 2 * d + 1 : d) * lt; }
+
+// Zw[tt][h][q][k] (h = 0: z0 or z, h = 1: dz = z1 - z0), then Zw[tt][2d][k] = |dz_k|^2 / 2 (increments)
+__global__ __launch_bounds__(256) void tvs_wide_prep_kernel(const float *__restrict__ Z, int lt, int t, int d, int incr,
+                                                            float *__restrict__ Zw) {
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long long)lt * t) return;
+  const int k = (int)(idx % lt), tt = (int)(idx / lt);
+  float *o = Zw + (long long)tt * tvs_wide_zs(d, lt, incr != 0);
+  if (!incr) {
+    const float *z = Z + ((long long)k * t + tt) * d;
+    for (int q = 0; q < d; ++q) o[(long long)q * lt + k] = z[q];
+  } else {
+    const float *z = Z + (((long long)k * t + tt) * 2) * d;
+    float h = 0.f;
+    for (int q = 0; q < d; ++q) {
+      const float dz = z[d + q] - z[q];
+      o[(long long)q * lt + k] = z[q];
+      o[((long long)d + q) * lt + k] = dz;
+      h = __builtin_fmaf(dz, dz, h);
+    }
+    o[(long long)2 * d * lt + k] = 0.5f * h;
+  }
+}
+
+template <int M, bool INCR, bool RBF>
+__global__ __launch_bounds__(64) void tvs_wide_kernel(TvsWideArgs a) {
+  constexpr int LT = M * (M + 1) / 2;
+  constexpr float TVS_CORNER = 2.0f;
+  constexpr float NHL2E = -0.72134752044448170f, L2E = 1.4426950408889634f;
+  constexpr int ANCHOR = GPSIG_TVS_ANCHOR;
+  const int lane = threadIdx.x;
+  const int tt = blockIdx.y;
+  const int n = a.n, d = a.d, FC = 2 * d + 3;
+  const int s0 = blockIdx.x * 64 + lane;
+  const int c0 = s0 < n ? s0 : n - 1;
+  cfloat *z0 = as_const(a.Zw) + (long long)tt * tvs_wide_zs(d, LT, INCR);  // [q][k]
+  cfloat *dz = z0 + (long long)d * LT;
+  cfloat *hdz = z0 + (long long)2 * d * LT;
+  auto ft = [&](int s, int c) { return a.Ft[((long long)s * FC + c) * n + c0]; };
+
+  // exact k(z0_k, x_s) and (INCR) expm1(p_k), p = -<z0 - x, dz> - |dz|^2/2, for every component
+  auto exact_all = [&](int s, float (&kc)[LT], float (&Ep)[LT]) {
+    float s2[LT], pp[LT];
+#pragma unroll
+    for (int k = 0; k < LT; ++k) s2[k] = pp[k] = 0.f;
+    for (int q = 0; q < d; ++q) {
+      const float xv = ft(s, q);
+#pragma unroll
+      for (int k = 0; k < LT; ++k) {
+        const float df = z0[(long long)q * LT + k] - xv;
+        s2[k] = __builtin_fmaf(df, df, s2[k]);
+        if constexpr (INCR) pp[k] = __builtin_fmaf(-df, dz[(long long)q * LT + k], pp[k]);
+      }
+    }
+#pragma unroll
+    for (int k = 0; k < LT; ++k) {
+      kc[k] = __builtin_amdgcn_exp2f(s2[k] * NHL2E);
+      if constexpr (INCR) {
+        const float p = pp[k] - hdz[k];
+        Ep[k] = __builtin_fabsf(p) < EM1_TAU ? em1_small(p) : __builtin_amdgcn_exp2f(p * L2E) - 1.0f;
+      }
+    }
+  };
+
+  float kc[LT], Ep[LT], Ss[LT], K[M + 1];
+#pragma unroll
+  for (int k = 0; k < LT; ++k) Ss[k] = Ep[k] = kc[k] = 0.f;
+#pragma unroll
+  for (int i = 0; i <= M; ++i) K[i] = 0.f;
+  if constexpr (RBF) exact_all(0, kc, Ep);
+
+  const int ncell = a.l - 1;
+  for (int s = 0; s < ncell; ++s) {
+    float qv[LT], cv[LT];
+    const float g = RBF ? ft(s, 2 * d + 1) : 0.f;
+#pragma unroll
+    for (int k = 0; k < LT; ++k) {
+      qv[k] = -g;
+      cv[k] = 0.f;
+    }
+    for (int q = 0; q < d; ++q) {
+      const float dxv = ft(s, d + q);
+#pragma unroll
+      for (int k = 0; k < LT; ++k) {
+        if constexpr (RBF) {
+          qv[k] = __builtin_fmaf(z0[(long long)q * LT + k], dxv, qv[k]);
+          if constexpr (INCR) cv[k] = __builtin_fmaf(dz[(long long)q * LT + k], dxv, cv[k]);
+        } else {  // linear: the seed is <w_k, dx_s>, w = z or z1 - z0
+          qv[k] = __builtin_fmaf(INCR ? dz[(long long)q * LT + k] : z0[(long long)q * LT + k], dxv, qv[k]);
+        }
+      }
+    }
+    float m[LT];
+    if constexpr (!RBF) {
+#pragma unroll
+      for (int k = 0; k < LT; ++k) m[k] = qv[k];
+    } else {
+      float mx = 0.f;
+#pragma unroll
+      for (int k = 0; k < LT; ++k) {
+        mx = __builtin_fmaxf(mx, __builtin_fabsf(qv[k]));
+        if constexpr (INCR) mx = __builtin_fmaxf(mx, __builtin_fabsf(cv[k]));
+      }
+      const bool wide = __builtin_amdgcn_ballot_w64(mx >= EM1_TAU) != 0;
+      const bool corner = INCR && wide && __builtin_amdgcn_ballot_w64(mx >= TVS_CORNER) != 0;
+      const bool anch = (s % ANCHOR) == ANCHOR - 1;
+      float Eq[LT], Ec[LT];
+#pragma unroll
+      for (int k = 0; k < LT; ++k) {
+        Eq[k] = em1_small(qv[k]);
+        Ec[k] = INCR ? em1_small(cv[k]) : 0.f;
+        if (wide) {
+          if (!(__builtin_fabsf(qv[k]) < EM1_TAU)) Eq[k] = __builtin_amdgcn_exp2f(qv[k] * L2E) - 1.0f;
+          if constexpr (INCR)
+            if (!(__builtin_fabsf(cv[k]) < EM1_TAU)) Ec[k] = __builtin_amdgcn_exp2f(cv[k] * L2E) - 1.0f;
+        }
+        if constexpr (INCR) {
+          float t = __builtin_fmaf(Ep[k], Ec[k], Ec[k]);
+          t = __builtin_fmaf(Eq[k], t, t);
+          m[k] = kc[k] * __builtin_fmaf(Ep[k], Eq[k], t);
+        } else {
+          m[k] = kc[k] * Eq[k];
+        }
+      }
+      if (corner) {
+        // increments far apart: corner differences of directly evaluated base-kernel values for the cells
+        // with |q| or |c| >= TVS_CORNER (z1 = z0 + dz)
+        float kn[LT], Epn[LT], e1[LT], e0[LT];
+        exact_all(s + 1, kn, Epn);
+#pragma unroll
+        for (int k = 0; k < LT; ++k) e1[k] = e0[k] = 0.f;
+        for (int q = 0; q < d; ++q) {
+          const float xs = ft(s, q), xn = ft(s + 1, q);
+#pragma unroll
+          for (int k = 0; k < LT; ++k) {
+            const float z1 = z0[(long long)q * LT + k] + dz[(long long)q * LT + k];
+            e1[k] = __builtin_fmaf(z1 - xn, z1 - xn, e1[k]);
+            e0[k] = __builtin_fmaf(z1 - xs, z1 - xs, e0[k]);
+          }
+        }
+#pragma unroll
+        for (int k = 0; k < LT; ++k) {
+          const bool ok = __builtin_fabsf(qv[k]) < TVS_CORNER && __builtin_fabsf(cv[k]) < TVS_CORNER;
+          const float k11 = __builtin_amdgcn_exp2f(e1[k] * NHL2E), k10 = __builtin_amdgcn_exp2f(e0[k] * NHL2E);
+          m[k] = ok ? m[k] : (k11 - k10) - (kn[k] - kc[k]);
+          kc[k] = kn[k];
+          Ep[k] = Epn[k];
+        }
+      } else if (anch) {
+        exact_all(s + 1, kc, Ep);  // re-anchor the recurrences every ANCHOR cells
+      } else {
+#pragma unroll
+        for (int k = 0; k < LT; ++k) {
+          if constexpr (INCR) {
+            kc[k] = __builtin_fmaf(kc[k], Eq[k], kc[k]);
+            Ep[k] = __builtin_fmaf(Ep[k], Ec[k], Ep[k] + Ec[k]);
+          } else {
+            kc[k] = kc[k] + m[k];
+          }
+        }
+      }
+    }
+    // the order-1 recursion (signature_algs.py:115-127), components in (level, stage) order
+#pragma unroll
+    for (int i = 1; i <= M; ++i) {
+      const int k0 = i * (i - 1) / 2;
+      float prev = m[k0];
+#pragma unroll
+      for (int st = 1; st < i; ++st) {
+        const float ss = Ss[k0 + st - 1];
+        Ss[k0 + st - 1] = ss + prev;
+        prev = m[k0 + st] * ss;
+      }
+      K[i] += prev;
+    }
+  }
+  if (s0 < n) {
+    a.out[(long long)tt * n + s0] = 1.0f;
+#pragma unroll
+    for (int i = 1; i <= M; ++i) a.out[((long long)i * a.t + tt) * n + s0] = K[i];
+    if (a.state) {
+#pragma unroll
+      for (int k = 0; k < LT; ++k) a.state[((long long)tt * n + s0) * LT + k] = Ss[k];
+    }
+  }
+}
+
+template <int M>
+static int launch_tvs_wide(const float *Z, int lt, int t, int incr, int d, const float *Ft, int n, int l, float *out,
+                           float *Zw, bool rbf, float *state, hipStream_t s) {
+  hipLaunchKernelGGL(tvs_wide_prep_kernel, dim3((unsigned)(((long long)lt * t + 255) / 256)), dim3(256), 0, s, Z, lt, t,
+                     d, incr, Zw);
+  TvsWideArgs a{Zw, Ft, t, n, l, d, out, state};
+  dim3 grid((unsigned)((n + 63) / 64), (unsigned)t);
+  if (rbf) {
+    if (incr) hipLaunchKernelGGL((tvs_wide_kernel<M, true, true>), grid, dim3(64), 0, s, a);
+    else hipLaunchKernelGGL((tvs_wide_kernel<M, false, true>), grid, dim3(64), 0, s, a);
+  } else {
+    if (incr) hipLaunchKernelGGL((tvs_wide_kernel<M, true, false>), grid, dim3(64), 0, s, a);
+    else hipLaunchKernelGGL((tvs_wide_kernel<M, false, false>), grid, dim3(64), 0, s, a);
+  }
+  return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
+}
+
+int tvs_wide_launch(const float *Z, int lt, int t, int increments, int d, const float *Ft, int n, int l, int M,
+                    float *out, float *Zw, bool rbf, float *state, hipStream_t s) {
+  if (l < 2) return -1;
+  switch (M) {
+    case 1: return launch_tvs_wide<1>(Z, lt, t, increments, d, Ft, n, l, out, Zw, rbf, state, s);
+    case 2: return launch_tvs_wide<2>(Z, lt, t, increments, d, Ft, n, l, out, Zw, rbf, state, s);
+    case 3: return launch_tvs_wide<3>(Z, lt, t, increments, d, Ft, n, l, out, Zw, rbf, state, s);
+    case 4: return launch_tvs_wide<4>(Z, lt, t, increments, d, Ft, n, l, out, Zw, rbf, state, s);
+    case 5: return launch_tvs_wide<5>(Z, lt, t, increments, d, Ft, n, l, out, Zw, rbf, state, s);
+    case 6: return launch_tvs_wide<6>(Z, lt, t, increments, d, Ft, n, l, out, Zw, rbf, state, s);
+    case 7: return launch_tvs_wide<7>(Z, lt, t, increments, d, Ft, n, l, out, Zw, rbf, state, s);
+    case 8: return launch_tvs_wide<8>(Z, lt, t, increments, d, Ft, n, l, out, Zw, rbf, state, s);
+    default: return -1;
+  }
+}
+
 template <int DP, int M, bool INCR>
 static int launch_tvs_pk(const float *Z, int lt, int t, int d, const float *Ft, int n, int l, float *out, float *Zp,
                          bool rbf, float *state, hipStream_t s) {
@@ -359,7 +594,8 @@ int tvs_pk_launch(const float *Z, int lt, int t, int increments, int d, const fl
 }
 
 size_t tvs_pk_zp_bytes(int lt, int t, int d) {
-  const int DP = d <= 2 ? 2 : d <= 4 ? 4 : d <= 6 ? 6 : 8;
+  // the packed paths' (T, LT, ZS) buffer (d <= 8) or the wide kernels' (T, 2d + 1, LT) one
+  const int DP = d <= 2 ? 2 : d <= 4 ? 4 : d <= 6 ? 6 : d <= 8 ? 8 : d;
   return ((size_t)lt * t * ((2 * DP + 2)) * sizeof(float) + 255) & ~(size_t)255;
 }
 

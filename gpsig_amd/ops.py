@@ -547,7 +547,8 @@ def tens_vs_seq_vjp(Z: torch.Tensor, X: torch.Tensor, num_levels: int, gout: tor
         gZ = torch.zeros(Z.shape, dtype=torch.float32, device=Z.device)
     if gX is None:
         gX = torch.zeros(X.shape, dtype=torch.float32, device=X.device)
-    ws = workspace(X.device, lib.gpsig_tens_vjp_workspace_bytes(n, l, d))
+    nb = lib.gpsig_tens_vjp_workspace_bytes(n, l, d) if d <= 16 else lib.gpsig_tens_vjp_wide_workspace_bytes(n, l, d, lt, t)
+    ws = workspace(X.device, nb)
     rc = lib.gpsig_tens_vs_seq_vjp(Z.data_ptr(), lt, t, int(increments), d, X.data_ptr(), n, l, num_levels,
                                    base_kind(base), int(bool(difference)), gout.data_ptr(), gZ.data_ptr(),
                                    gX.data_ptr(), _ptr(state), ws.data_ptr(),

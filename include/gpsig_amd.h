@@ -185,13 +185,16 @@ int gpsig_tens_vs_seq_state(const float *Z, int lt, int t, int increments, int d
                             int num_levels, int base_kind, float *out, float *state, void *workspace,
                             size_t workspace_bytes, gpsig_stream_t stream);
 
-/* Gradient of gpsig_tens_vs_seq (order 1, difference 1 or 0, RBF or linear, num_levels <= 8, d <= 16):
+/* Gradient of gpsig_tens_vs_seq (order 1, difference 1 or 0, RBF or linear, num_levels <= 8, any d):
  * the reference differentiates _K_tens_vs_seq (kernels.py:314-341 + signature_algs.py:101-127) by TF
  * autodiff.  gout (num_levels+1, T, n) = dLoss/d(raw per-level output); accumulates (+=) gZ (same
  * layout as Z) and gX (n, l, d).  state: NULL, or the buffer a gpsig_tens_vs_seq_state call on the same
  * inputs filled (difference 1): the VJP then skips its forward sweep.  Workspace:
- * gpsig_tens_vjp_workspace_bytes(n, l, d). */
+ * gpsig_tens_vjp_workspace_bytes(n, l, d) for d <= 16, gpsig_tens_vjp_wide_workspace_bytes(...) above. */
 size_t gpsig_tens_vjp_workspace_bytes(int n, int l, int d);
+/* Workspace of gpsig_tens_vs_seq_vjp at d > 16 (point-weight tiles of a chunk of sequences and the emission
+ * GEMMs on the matrix cores; any channel count). */
+size_t gpsig_tens_vjp_wide_workspace_bytes(int n, int l, int d, int lt, int t);
 
 int gpsig_tens_vs_seq_vjp(const float *Z, int lt, int t, int increments, int d, const float *X, int n, int l,
                           int num_levels, int base_kind, int difference, const float *gout, float *gZ, float *gX,
