@@ -62,6 +62,14 @@ SIGNATURES = {
     "gpsig_pde_fronts": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _SZ, _P]),
     "gpsig_pde_vjp_fronts": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _SZ, _P]),
     "gpsig_sym_assemble": (_I, [_P, _P, ctypes.c_longlong, _I, _I, _P, _P]),
+    "gpsig_pde_scratch_bytes": (_SZ, [_I, _I, _I, _I, _I, _I, _I]),
+    "gpsig_pde_gram_ex": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _I, _I, _P, _SZ, _P]),
+    "gpsig_pde_diag_ex": (_I, [_P, _I, _I, _I, _I, _I, _P, _P, _SZ, _P]),
+    "gpsig_pde_vjp_scratch_bytes": (_SZ, [_I, _I, _I, _I, _I, _I, _I]),
+    "gpsig_pde_vjp_ex": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _SZ, _P, _SZ, _P]),
+    "gpsig_pde_fronts_ex": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _SZ, _P, _SZ, _P]),
+    "gpsig_pde_vjp_fronts_ex": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _SZ, _P, _SZ,
+                                     _P]),
     "gpsig_tens_vs_seq": (_I, [_P, _I, _I, _I, _I, _P, _I, _I, _I, _I, _I, _I, _P, _P, _SZ, _P]),
     "gpsig_tens_gram": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P]),
     "gpsig_tens_vs_seq_vjp": (_I, [_P, _I, _I, _I, _I, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _SZ, _P]),

@@ -17,6 +17,11 @@ int pde_launch(const float *X, int n1, int l1, const float *Y, int n2, int l2, i
                long long out_ld, hipStream_t s);
 int sym_assemble_launch(const float *src, const long long *row_off, long long level_stride, int n, int levels,
                         float *dst, hipStream_t s);
+bool pde_tiled(int d, int dyadic);
+size_t pde_tile_scratch_bytes(int n1, int l1, int n2, int l2, int d, int pair_mode);
+int pde_launch_tiled(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int dyadic, int solver,
+                     int pair_mode, int row_begin, int row_end, float *out, int out_row0, int out_rows,
+                     long long out_ld, void *scratch, size_t scratch_bytes, hipStream_t s);
 }  // namespace gpsig
 
 using namespace gpsig;
@@ -204,22 +209,43 @@ extern "C" int gpsig_sig_diag(const float *X, int n, int l, int d, int num_level
                         nullptr, nullptr, nullptr, jitter, out_mode, out, 0, n, workspace, workspace_bytes, stream);
 }
 
-extern "C" int gpsig_pde_gram(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int dyadic,
-                              int solver, int pair_mode, int row_begin, int row_end, float *out, int out_row0,
-                              int out_rows, gpsig_stream_t stream) {
+extern "C" size_t gpsig_pde_scratch_bytes(int n1, int l1, int n2, int l2, int d, int dyadic, int pair_mode) {
+  if (!pde_tiled(d, dyadic)) return 0;
+  return pde_tile_scratch_bytes(n1, l1, n2, l2, d, pair_mode);
+}
+
+extern "C" int gpsig_pde_gram_ex(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int dyadic,
+                                 int solver, int pair_mode, int row_begin, int row_end, float *out, int out_row0,
+                                 int out_rows, void *scratch, size_t scratch_bytes, gpsig_stream_t stream) {
   if (!X || !Y || !out || n1 <= 0 || n2 <= 0 || d <= 0 || l1 < 2 || l2 < 2) return GPSIG_EINVAL;
-  if (dyadic < 0 || dyadic > 6 || (solver != 0 && solver != 1)) return GPSIG_EINVAL;
+  if (dyadic < 0 || dyadic > 8 || (solver != 0 && solver != 1)) return GPSIG_EINVAL;
   if (pair_mode < GPSIG_PAIRS_RECT || pair_mode > GPSIG_PAIRS_DIAG) return GPSIG_EINVAL;
   if (row_begin < 0 || row_end > n1 || row_begin > row_end) return GPSIG_EINVAL;
   if (pair_mode != GPSIG_PAIRS_RECT && (n1 != n2 || l1 != l2)) return GPSIG_EINVAL;
   if (row_end == row_begin) return GPSIG_OK;
+  if (pde_tiled(d, dyadic))
+    return pde_launch_tiled(X, n1, l1, Y, n2, l2, d, dyadic, solver, pair_mode, row_begin, row_end, out, out_row0,
+                            out_rows, n2, scratch, scratch_bytes, reinterpret_cast<hipStream_t>(stream));
   return pde_launch(X, n1, l1, Y, n2, l2, d, dyadic, solver, pair_mode, row_begin, row_end, out, out_row0,
                     out_rows, n2, reinterpret_cast<hipStream_t>(stream));
 }
 
+extern "C" int gpsig_pde_gram(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int dyadic,
+                              int solver, int pair_mode, int row_begin, int row_end, float *out, int out_row0,
+                              int out_rows, gpsig_stream_t stream) {
+  return gpsig_pde_gram_ex(X, n1, l1, Y, n2, l2, d, dyadic, solver, pair_mode, row_begin, row_end, out, out_row0,
+                           out_rows, nullptr, 0, stream);
+}
+
+extern "C" int gpsig_pde_diag_ex(const float *X, int n, int l, int d, int dyadic, int solver, float *out,
+                                 void *scratch, size_t scratch_bytes, gpsig_stream_t stream) {
+  return gpsig_pde_gram_ex(X, n, l, X, n, l, d, dyadic, solver, GPSIG_PAIRS_DIAG, 0, n, out, 0, n, scratch,
+                           scratch_bytes, stream);
+}
+
 extern "C" int gpsig_pde_diag(const float *X, int n, int l, int d, int dyadic, int solver, float *out,
                               gpsig_stream_t stream) {
-  return gpsig_pde_gram(X, n, l, X, n, l, d, dyadic, solver, GPSIG_PAIRS_DIAG, 0, n, out, 0, n, stream);
+  return gpsig_pde_diag_ex(X, n, l, d, dyadic, solver, out, nullptr, 0, stream);
 }
 
 extern "C" int gpsig_sym_assemble(const float *src, const long long *row_off, long long level_stride, int n,

@@ -28,7 +28,21 @@ struct PdeArgs {
   float *out;
   int out_row0, out_rows;
   long long out_ld;
+  // DP == 0 (increment tiles, any channel count): the coarse increment Gram <dx_i, dy_j> of pair (a, b)
+  // at inc + (a - inc_a0) inc_as + (b - inc_b0) (l2 - 1) + i inc_ld + j (DIAG: + i inc_ld + j), computed
+  // by the matrix-core GEMM (gemm.hip) -- the reference's own split (kernels_pde.py:176 tf.matmul, then
+  // the solver).  sub > 0: the kernel's grid is 2^sub times finer than the tile (each tile cell covers
+  // 2^sub x 2^sub kernel cells, value / 4^sub).
+  const float *inc;
+  long long inc_as, inc_ld;
+  int inc_a0, inc_b0, sub;
 };
+
+// increment of kernel cell (ci, cj) from the tile (DP == 0 kernels)
+GPSIG_DEV float tile_inc(const float *__restrict__ base, long long ld, int sub, int ci, int cj) {
+  const float v = base[(long long)(ci >> sub) * ld + (cj >> sub)];
+  return sub ? v * __builtin_ldexpf(1.0f, -2 * sub) : v;
+}
 
 template <typename T, int DP, int W>
 __global__ __launch_bounds__(256) void pde_kernel(PdeArgs p) {
@@ -167,6 +181,8 @@ template <typename T, int DP, int W, int REP, int SOLVER, int LP = 64>
 __global__ __launch_bounds__(256) void pde_rep_kernel(PdeArgs p) {
   static_assert(W % REP == 0, "a lane owns whole coarse columns");
   static_assert(LP == 16 || LP == 32 || LP == 64, "lane group");
+  constexpr bool TILE = DP == 0;  // increments from the tile (any channel count)
+  constexpr int DPA = TILE ? 1 : DP;
   constexpr int WC = W / REP;
   constexpr int G = 64 / LP;
   constexpr int CB = LP * W;  // fine columns per block (G > 1: one block)
@@ -201,7 +217,8 @@ __global__ __launch_bounds__(256) void pde_rep_kernel(PdeArgs p) {
   if (!bok) b = p.pair_mode == GPSIG_PAIRS_RECT ? 0 : a;
 
   const T inv_factor = (T)1.0 / (T)(REP * REP);
-  const int IC = p.l1 - 1, JC = p.l2 - 1;  // coarse rows / columns
+  // coarse rows / columns (TILE with sub > 0: the tile's cells split 2^sub ways per direction)
+  const int IC = (p.l1 - 1) << (TILE ? p.sub : 0), JC = (p.l2 - 1) << (TILE ? p.sub : 0);
   const int I = REP * IC, J = REP * JC;
   const int nblk = (J + CB - 1) / CB;
   const int d = p.d;
@@ -209,12 +226,19 @@ __global__ __launch_bounds__(256) void pde_rep_kernel(PdeArgs p) {
   const float *y = p.Y + (long long)b * p.l2 * d;
 
   float *dxs = lds + (size_t)wave * IC * DP;
-  for (int r = lane; r < IC; r += 64)
+  if constexpr (!TILE) {
+    for (int r = lane; r < IC; r += 64)
 #pragma unroll
-    for (int k = 0; k < DP; ++k) dxs[r * DP + k] = k < d ? x[(r + 1) * d + k] - x[r * d + k] : 0.0f;
+      for (int k = 0; k < DP; ++k) dxs[r * DP + k] = k < d ? x[(r + 1) * d + k] - x[r * d + k] : 0.0f;
+  }
   T *bnd = reinterpret_cast<T *>(lds + (((size_t)4 * IC * DP + 3) & ~(size_t)3)) + (size_t)wave * (I + 1);
   __syncthreads();
   if (!aok || (G == 1 && !ok)) return;
+  // this pair's increment tile (TILE)
+  const float *__restrict__ itile =
+      TILE ? p.inc + (long long)(a - p.inc_a0) * p.inc_as +
+                 (p.pair_mode == GPSIG_PAIRS_DIAG ? 0 : (long long)(b - p.inc_b0) * (p.l2 - 1))
+           : nullptr;
 
   const bool hybrid = (p.pair_mode == GPSIG_PAIRS_DIAG) && SOLVER == 0;
   constexpr bool s1 = SOLVER == 1;
@@ -226,13 +250,15 @@ __global__ __launch_bounds__(256) void pde_rep_kernel(PdeArgs p) {
     const int c0 = blk * CB;  // first fine column of the block (a multiple of REP)
     const bool from_left = blk > 0, to_right = blk + 1 < nblk;
     // y increments of this lane's coarse columns
-    f2 dy[WC2][DP];
+    f2 dy[WC2][DPA];
+    if constexpr (!TILE) {
 #pragma unroll
-    for (int w = 0; w < 2 * WC2; ++w) {
-      int cj = c0 / REP + gl * WC + w;
-      cj = cj < JC - 1 ? cj : JC - 1;
+      for (int w = 0; w < 2 * WC2; ++w) {
+        int cj = c0 / REP + gl * WC + w;
+        cj = cj < JC - 1 ? cj : JC - 1;
 #pragma unroll
-      for (int k = 0; k < DP; ++k) dy[w / 2][k][w % 2] = (k < d && w < WC) ? y[(cj + 1) * d + k] - y[cj * d + k] : 0.0f;
+        for (int k = 0; k < DP; ++k) dy[w / 2][k][w % 2] = (k < d && w < WC) ? y[(cj + 1) * d + k] - y[cj * d + k] : 0.0f;
+      }
     }
 #pragma unroll
     for (int w = 0; w < W; ++w) up[w] = (T)1;
@@ -251,17 +277,27 @@ __global__ __launch_bounds__(256) void pde_rep_kernel(PdeArgs p) {
       }
       const int ci = s - gl;
       if (ci >= 0 && ci < IC && gl < lanes_used) {
+        f2 incp[WC2];
+        if constexpr (TILE) {
+          // the tile's coarse increments (columns past the sequence read its last column: never a real cell)
+#pragma unroll
+          for (int w = 0; w < 2 * WC2; ++w) {
+            int cj = c0 / REP + gl * WC + w;
+            cj = cj < JC - 1 ? cj : JC - 1;
+            incp[w / 2][w % 2] = w < WC ? tile_inc(itile, p.inc_ld, p.sub, ci, cj) : 0.0f;
+          }
+        } else {
         const float *dxr = dxs + ci * DP;
         float dxv[DP];
 #pragma unroll
         for (int k = 0; k < DP; ++k) dxv[k] = dxr[k];
-        f2 incp[WC2];
 #pragma unroll
         for (int w2 = 0; w2 < WC2; ++w2) {
           f2 acc = dy[w2][0] * splat2(dxv[0]);
 #pragma unroll
           for (int k = 1; k < DP; ++k) acc = fma2(dy[w2][k], splat2(dxv[k]), acc);
           incp[w2] = acc;
+        }
         }
         // coefficients of the lane's coarse cells: solver 1 uses (A, B), solver 0 uses inc - 1 (as B)
         T A[WC], B[WC];
@@ -408,15 +444,17 @@ static int pde_lp_dispatch(const PdeArgs &a, long long nblocks, PdeLp g, hipStre
   return GPSIG_EUNSUPPORTED;
 }
 
-// W = the smallest multiple of REP with J / W <= 64 lanes (-1: use the per-row kernel)
+// W = the smallest multiple of REP with J / W <= 64 lanes (-1: use the per-row kernel).  Longer grids run
+// in column blocks of 64 W fine columns: W = 4 REP for REP <= 4, 16 for REP = 8 and 16 (dyadic 3 and 4).
 template <typename T, int DP, int REP>
 static int pde_rep_w(const PdeArgs &a, long long nblocks, int J, hipStream_t s) {
   if (J <= 64 * REP) return launch_pde_rep<T, DP, REP, REP>(a, nblocks, s);
   if (J <= 128 * REP && 2 * REP <= 16) return launch_pde_rep<T, DP, (2 * REP <= 16 ? 2 * REP : REP), REP>(a, nblocks, s);
   if (REP <= 4 && J <= 192 * REP) return launch_pde_rep<T, DP, (REP <= 4 ? 3 * REP : REP), REP>(a, nblocks, s);
   if (REP <= 4 && J <= 256 * REP) return launch_pde_rep<T, DP, (REP <= 4 ? 4 * REP : REP), REP>(a, nblocks, s);
-  // longer: column blocks of 256 * REP fine columns
+  // longer: column blocks of 256 * REP fine columns (REP <= 4) or 1024 (REP 8, 16)
   if (REP <= 4) return launch_pde_rep<T, DP, (REP <= 4 ? 4 * REP : REP), REP>(a, nblocks, s);
+  if (REP <= 16) return launch_pde_rep<T, DP, 16, (REP <= 16 ? REP : 16)>(a, nblocks, s);
   return -1;
 }
 
@@ -434,41 +472,47 @@ static int launch_pde(const PdeArgs &a, long long nblocks, hipStream_t s) {
 
 template <typename T, int DP>
 static int pde_w(const PdeArgs &a, long long nblocks, int J, PdeLp g, hipStream_t s) {
-  if (g.LP != 64) {
-    if (a.dyadic == 0) return pde_lp_dispatch<T, DP, 1>(a, nblocks, g, s);
-    if (a.dyadic == 1) return pde_lp_dispatch<T, DP, 2>(a, nblocks, g, s);
-    if (a.dyadic == 2) return pde_lp_dispatch<T, DP, 4>(a, nblocks, g, s);
-    return GPSIG_EUNSUPPORTED;
+  if constexpr (DP > 0) {
+    if (g.LP != 64) {
+      if (a.dyadic == 0) return pde_lp_dispatch<T, DP, 1>(a, nblocks, g, s);
+      if (a.dyadic == 1) return pde_lp_dispatch<T, DP, 2>(a, nblocks, g, s);
+      if (a.dyadic == 2) return pde_lp_dispatch<T, DP, 4>(a, nblocks, g, s);
+      return GPSIG_EUNSUPPORTED;
+    }
   }
   {
+    // kernel grid 2^(dyadic - sub) (TILE with sub > 0: the tile is 2^sub coarser than the kernel's cells)
+    const int kd = a.dyadic - a.sub;
     int rc = -1;
-    if (a.dyadic == 0) rc = pde_rep_w<T, DP, 1>(a, nblocks, J, s);
-    if (a.dyadic == 1) rc = pde_rep_w<T, DP, 2>(a, nblocks, J, s);
-    if (a.dyadic == 2) rc = pde_rep_w<T, DP, 4>(a, nblocks, J, s);
+    if (kd == 0) rc = pde_rep_w<T, DP, 1>(a, nblocks, J, s);
+    if (kd == 1) rc = pde_rep_w<T, DP, 2>(a, nblocks, J, s);
+    if (kd == 2) rc = pde_rep_w<T, DP, 4>(a, nblocks, J, s);
+    if (kd == 3) rc = pde_rep_w<T, DP, 8>(a, nblocks, J, s);
+    if (kd == 4) rc = pde_rep_w<T, DP, 16>(a, nblocks, J, s);
     if (rc != -1) return rc;
   }
-  if (J <= 64) return launch_pde<T, DP, 1>(a, nblocks, s);
-  if (J <= 128) return launch_pde<T, DP, 2>(a, nblocks, s);
-  if (J <= 256) return launch_pde<T, DP, 4>(a, nblocks, s);
-  if (J <= 512) return launch_pde<T, DP, 8>(a, nblocks, s);
-  if (J <= 1024) return launch_pde<T, DP, 16>(a, nblocks, s);
-  return GPSIG_EUNSUPPORTED;
+  if constexpr (DP == 0) {
+    return GPSIG_EUNSUPPORTED;
+  } else {
+    if (J <= 64) return launch_pde<T, DP, 1>(a, nblocks, s);
+    if (J <= 128) return launch_pde<T, DP, 2>(a, nblocks, s);
+    if (J <= 256) return launch_pde<T, DP, 4>(a, nblocks, s);
+    if (J <= 512) return launch_pde<T, DP, 8>(a, nblocks, s);
+    if (J <= 1024) return launch_pde<T, DP, 16>(a, nblocks, s);
+    return GPSIG_EUNSUPPORTED;
+  }
 }
 
-int pde_launch(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int dyadic, int solver,
-               int pair_mode, int row_begin, int row_end, float *out, int out_row0, int out_rows,
-               long long out_ld, hipStream_t s) {
-  PdeArgs a{};
-  a.X = X; a.Y = Y;
-  a.n1 = n1; a.l1 = l1; a.n2 = n2; a.l2 = l2; a.d = d;
-  a.dyadic = dyadic; a.solver = solver;
-  a.pair_mode = pair_mode; a.row_begin = row_begin; a.row_end = row_end;
-  a.out = out; a.out_row0 = out_row0; a.out_rows = out_rows; a.out_ld = out_ld;
+// a: inputs, mode, rows and output filled; a.inc != nullptr selects the increment-tile kernels (DP == 0)
+static int pde_launch_args(PdeArgs a, hipStream_t s) {
+  const int n2 = a.n2, l1 = a.l1, l2 = a.l2, d = a.d, dyadic = a.dyadic, solver = a.solver;
+  const int pair_mode = a.pair_mode, row_begin = a.row_begin, row_end = a.row_end;
+  const bool tile = a.inc != nullptr;
   const int J = (1 << dyadic) * (l2 - 1);
   const int DPI = d <= 8 ? d : 16;
   // lane groups of Gram pairs: solver 1, dyadic <= 2, d <= 8 (pde_pick_lp)
   PdeLp lpg{64, 0};
-  if (pair_mode != GPSIG_PAIRS_DIAG && solver == 1 && dyadic <= 2 && d <= 8 && l1 >= 2 && l2 >= 2)
+  if (!tile && pair_mode != GPSIG_PAIRS_DIAG && solver == 1 && dyadic <= 2 && d <= 8 && l1 >= 2 && l2 >= 2)
     lpg = pde_pick_lp(l1 - 1, J, 1 << dyadic, DPI);
   const int G = 64 / lpg.LP;
   long long nblocks;
@@ -489,7 +533,9 @@ int pde_launch(const float *X, int n1, int l1, const float *Y, int n2, int l2, i
     }
   }
   if (nblocks <= 0) return GPSIG_OK;
+  if (nblocks > 0x7fffffffLL) return GPSIG_EUNSUPPORTED;
   using T = double;  // fp64 solution grid (the reference's float64), fp32 increments (as the CUDA op, .cu:27)
+  if (tile) return pde_w<T, 0>(a, nblocks, J, lpg, s);
   switch (d <= 8 ? d : (d <= 16 ? 16 : 0)) {
 #define CASE(v) \
   case v: return pde_w<T, v>(a, nblocks, J, lpg, s);
@@ -497,6 +543,138 @@ int pde_launch(const float *X, int n1, int l1, const float *Y, int n2, int l2, i
 #undef CASE
     default: return GPSIG_EUNSUPPORTED;
   }
+}
+
+int pde_launch(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int dyadic, int solver,
+               int pair_mode, int row_begin, int row_end, float *out, int out_row0, int out_rows,
+               long long out_ld, hipStream_t s) {
+  PdeArgs a{};
+  a.X = X; a.Y = Y;
+  a.n1 = n1; a.l1 = l1; a.n2 = n2; a.l2 = l2; a.d = d;
+  a.dyadic = dyadic; a.solver = solver;
+  a.pair_mode = pair_mode; a.row_begin = row_begin; a.row_end = row_end;
+  a.out = out; a.out_row0 = out_row0; a.out_rows = out_rows; a.out_ld = out_ld;
+  return pde_launch_args(a, s);
+}
+
+// ------------------------------------------------------------------------------------ increment tiles
+int gemm_f32(hipStream_t s, bool transA, bool transB, int M, int N, int K, float alpha, const float *A, long long lda,
+             long long sA, const float *B, long long ldb, long long sB, float beta, float *C, long long ldc,
+             long long sC, int batch, int skip_rb, int skip_cb, float *partial);
+
+// dX[a][i][k] = x[a][i+1][k] - x[a][i][k]: the coarse increments, (n, l-1, d) row-major
+__global__ __launch_bounds__(256) void increments_kernel(const float *__restrict__ X, int n, int l, int d,
+                                                         float *__restrict__ dX) {
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long long)n * (l - 1) * d) return;
+  const int k = (int)(idx % d);
+  const long long r = idx / d;
+  const long long a = r / (l - 1), i = r % (l - 1);
+  const float *x = X + (a * l + i) * d + k;
+  dX[idx] = x[d] - x[0];
+}
+int increments_launch(const float *X, int n, int l, int d, float *dX, hipStream_t s) {
+  const long long tot = (long long)n * (l - 1) * d;
+  hipLaunchKernelGGL(increments_kernel, dim3((unsigned)((tot + 255) / 256)), dim3(256), 0, s, X, n, l, d, dX);
+  return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
+}
+
+static size_t al256p(size_t b) { return (b + 255) & ~(size_t)255; }
+constexpr size_t PDE_TILE_BYTES = (size_t)1 << 30;  // increment tile of one chunk of x-rows
+
+// x-rows per chunk of the tiled path (a multiple of 4) and the tile's row length
+static void pde_tile_chunk(int n1, int l1, int n2, int l2, int pair_mode, int &rows, long long &cols) {
+  cols = pair_mode == GPSIG_PAIRS_DIAG ? (long long)(l1 - 1) : (long long)n2 * (l2 - 1);
+  long long r = (long long)(PDE_TILE_BYTES / ((size_t)(l1 - 1) * cols * sizeof(float)));
+  r = r < 4 ? 4 : (r / 4) * 4;
+  if (r > ((n1 + 3) / 4) * 4) r = ((n1 + 3) / 4) * 4;
+  rows = (int)r;
+}
+
+// The increment-tile path needs a scratch buffer; 0 when the fixed-channel kernels apply.
+bool pde_tiled(int d, int dyadic) { return d > 16 || dyadic > 4; }
+size_t pde_tile_scratch_bytes(int n1, int l1, int n2, int l2, int d, int pair_mode) {
+  if (n1 <= 0 || n2 <= 0 || l1 < 2 || l2 < 2 || d <= 0) return 0;
+  int rows;
+  long long cols;
+  pde_tile_chunk(n1, l1, n2, l2, pair_mode, rows, cols);
+  const bool same = pair_mode != GPSIG_PAIRS_RECT;
+  return al256p((size_t)n1 * (l1 - 1) * d * sizeof(float)) +
+         (same ? 0 : al256p((size_t)n2 * (l2 - 1) * d * sizeof(float))) +
+         al256p((size_t)rows * (l1 - 1) * cols * sizeof(float));
+}
+
+// Increment tiles of chunks of x-rows (one matrix-core GEMM each: dX_chunk dY^T, or per pair for DIAG),
+// each followed by the tile-fed solver launch.  prep(a, c0, r1) fills the launch's rows and mode fields.
+int pde_tiled_run(PdeArgs a, void *scratch, size_t scratch_bytes, hipStream_t s,
+                  int (*launch)(PdeArgs, hipStream_t, void *), void *ctx) {
+  const int n1 = a.n1, l1 = a.l1, n2 = a.n2, l2 = a.l2, d = a.d, pm = a.pair_mode;
+  const int IC = l1 - 1, JC = l2 - 1;
+  if (!scratch || scratch_bytes < pde_tile_scratch_bytes(n1, l1, n2, l2, d, pm)) return GPSIG_EWORKSPACE;
+  int rows;
+  long long cols;
+  pde_tile_chunk(n1, l1, n2, l2, pm, rows, cols);
+  char *w = static_cast<char *>(scratch);
+  float *dX = reinterpret_cast<float *>(w);
+  w += al256p((size_t)n1 * IC * d * sizeof(float));
+  float *dY = dX;
+  if (pm == GPSIG_PAIRS_RECT) {
+    dY = reinterpret_cast<float *>(w);
+    w += al256p((size_t)n2 * JC * d * sizeof(float));
+  }
+  float *T = reinterpret_cast<float *>(w);
+  int rc = increments_launch(a.X, n1, l1, d, dX, s);
+  if (rc) return rc;
+  if (pm == GPSIG_PAIRS_RECT && (rc = increments_launch(a.Y, n2, l2, d, dY, s))) return rc;
+  // kernel grid: 2^(dyadic - sub) fine cells per tile cell and direction (pde_rep_w takes up to 16)
+  a.sub = a.dyadic > 4 ? a.dyadic - 4 : 0;
+  a.inc = T;
+  const int rb0 = a.row_begin, rb1 = a.row_end;
+  for (int r0 = (rb0 / 4) * 4; r0 < rb1; r0 += rows) {
+    const int r1 = r0 + rows < rb1 ? r0 + rows : rb1;
+    const int c0 = r0 > rb0 ? r0 : rb0;
+    PdeArgs c = a;
+    c.row_begin = c0;
+    c.row_end = r1;
+    if (pm == GPSIG_PAIRS_DIAG) {
+      c.inc_a0 = c0;
+      c.inc_b0 = 0;
+      c.inc_as = (long long)IC * IC;
+      c.inc_ld = IC;
+      rc = gemm_f32(s, false, true, IC, IC, d, 1.0f, dX + (long long)c0 * IC * d, d, (long long)IC * d,
+                    dX + (long long)c0 * IC * d, d, (long long)IC * d, 0.0f, T, IC, (long long)IC * IC, r1 - c0, 0, 0,
+                    nullptr);
+    } else {
+      const int b0 = pm == GPSIG_PAIRS_UPPER ? r0 : 0;
+      const long long tc = (long long)(n2 - b0) * JC;
+      c.inc_a0 = r0;
+      c.inc_b0 = b0;
+      c.inc_as = (long long)IC * tc;
+      c.inc_ld = tc;
+      // UPPER: tiles whose x-rows all lie past their y-columns are never read (b >= a)
+      rc = gemm_f32(s, false, true, (r1 - r0) * IC, (int)tc, d, 1.0f, dX + (long long)r0 * IC * d, d, 0,
+                    dY + (long long)b0 * JC * d, d, 0, 0.0f, T, tc, 0, 1, pm == GPSIG_PAIRS_UPPER ? IC : 0,
+                    pm == GPSIG_PAIRS_UPPER ? JC : 0, nullptr);
+    }
+    if (rc) return rc;
+    if ((rc = launch(c, s, ctx))) return rc;
+  }
+  return GPSIG_OK;
+}
+
+static int pde_fwd_launch_cb(PdeArgs a, hipStream_t s, void *) { return pde_launch_args(a, s); }
+
+// gpsig_pde_gram through the increment tiles (any channel count, any dyadic order)
+int pde_launch_tiled(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int dyadic, int solver,
+                     int pair_mode, int row_begin, int row_end, float *out, int out_row0, int out_rows,
+                     long long out_ld, void *scratch, size_t scratch_bytes, hipStream_t s) {
+  PdeArgs a{};
+  a.X = X; a.Y = Y;
+  a.n1 = n1; a.l1 = l1; a.n2 = n2; a.l2 = l2; a.d = d;
+  a.dyadic = dyadic; a.solver = solver;
+  a.pair_mode = pair_mode; a.row_begin = row_begin; a.row_end = row_end;
+  a.out = out; a.out_row0 = out_row0; a.out_rows = out_rows; a.out_ld = out_ld;
+  return pde_tiled_run(a, scratch, scratch_bytes, s, pde_fwd_launch_cb, nullptr);
 }
 
 // ------------------------------------------------------------------------------------ assembly

@@ -47,9 +47,23 @@ struct PdeBwdArgs {
   float *fronts;      // workspace: per evaluated pair, nfronts x (W + REP) x 64 floats (pde_front_floats)
   float *out;         // MODE 1 (forward with fronts): K per pair, DIAG out[a - row_begin], RECT
                       // out[(a - row_begin) * n2 + b]
+  // DP == 0 (any channel count; dyadic > 3): increments from the tile of the pair (as PdeArgs: inc +
+  // (a - inc_a0) inc_as + (b - inc_b0) (l2 - 1) + i inc_ld + j, kernel cells 2^sub finer than the tile),
+  // and the adjoint's coarse-cell sums go to the tile gt of the same layout, scaled to dLoss/d<dx_i, dy_j>
+  // (the host contracts them with the increments in two GEMMs)
+  const float *inc;
+  float *gt;
+  long long inc_as, inc_ld;
+  int inc_a0, inc_b0, sub;
 };
 
 GPSIG_DEV double lane_next_d(double v) { return dpp_d<0x130>(v); }
+
+// increment of kernel cell (ci, cj) from the pair's tile (tile cells 2^sub times coarser, value / 4^sub)
+GPSIG_DEV float tile_inc_b(const float *__restrict__ base, long long ld, int sub, int ci, int cj) {
+  const float v = base[(long long)(ci >> sub) * ld + (cj >> sub)];
+  return sub ? v * __builtin_ldexpf(1.0f, -2 * sub) : v;
+}
 
 // coarse steps per stored front: the chunk's K corners (H x REP x W floats per lane) live in registers
 template <int W, int REP>
@@ -92,8 +106,17 @@ __host__ __device__ inline PdeLayout pde_layout(int l1, int l2, int dyadic) {
   L.pair_floats = L.kb_off + (L.nblk > 1 ? 2LL * L.nblk * (IC * rep + 1) : 0);
   return L;
 }
+// Past dyadic 3 the adjoint runs on the increment tiles with kernel cells 2^(dyadic - 3) finer than the
+// coarse grid (pde_bwd_sub): the layout of that grid.
+__host__ __device__ inline int pde_bwd_sub(int dyadic) { return dyadic > 3 ? dyadic - 3 : 0; }
+__host__ __device__ inline PdeLayout pde_layout_eff(int l1, int l2, int dyadic) {
+  const int sub = pde_bwd_sub(dyadic);
+  if (sub == 0) return pde_layout(l1, l2, dyadic);
+  if (((long long)(l1 - 1) << sub) > (1 << 24) || ((long long)(l2 - 1) << sub) > (1 << 24)) return PdeLayout{};
+  return pde_layout(((l1 - 1) << sub) + 1, ((l2 - 1) << sub) + 1, 3);
+}
 // fp32 words of the adjoint's workspace for one pair (0: unsupported)
-inline long long pde_front_floats(int l1, int l2, int dyadic) { return pde_layout(l1, l2, dyadic).pair_floats; }
+inline long long pde_front_floats(int l1, int l2, int dyadic) { return pde_layout_eff(l1, l2, dyadic).pair_floats; }
 
 // LDS of one wave (pair) of the adjoint kernel, in doubles
 __host__ __device__ inline size_t pde_lds_wave_doubles(int IC, int DP) { return ((size_t)IC * DP * 12 + 7) / 8; }
@@ -112,6 +135,8 @@ GPSIG_DEV double ld_l2_d(const double *p) { return __hip_atomic_load(p, __ATOMIC
 template <int DP, int W, int REP, bool COLS, int MODE = 0>
 __global__ __launch_bounds__(256) void pde_adj_kernel(PdeBwdArgs p) {
   static_assert(W % REP == 0, "a lane owns whole coarse columns");
+  constexpr bool TILE = DP == 0;
+  constexpr int DPA = TILE ? 1 : DP;
   constexpr int WC = W / REP;
   constexpr int H = pde_chunk<W, REP>();
   constexpr int FW = W + REP;  // front words per lane: up[W], last[0 .. REP-2], corner_prev
@@ -132,13 +157,17 @@ __global__ __launch_bounds__(256) void pde_adj_kernel(PdeBwdArgs p) {
   if (!ok) { a = p.row_begin; b = diag ? a : 0; }
 
   const double inv_factor = 1.0 / (double)(REP * REP);
-  const int IC = p.l1 - 1, JC = p.l2 - 1;
+  const int sub = TILE ? p.sub : 0;
+  const int IC = (p.l1 - 1) << sub, JC = (p.l2 - 1) << sub;
   const int J = JC * REP, I = IC * REP;
   const int d = p.d;
   const float *x = p.X + (long long)a * p.l1 * d;
   const float *y = p.Y + (long long)b * p.l2 * d;
   const long long pidx = diag ? (long long)(a - p.row_begin) : (long long)(a - p.row_begin) * p.n2 + b;
-  const PdeLayout lay = pde_layout(p.l1, p.l2, p.dyadic);
+  const PdeLayout lay = pde_layout_eff(p.l1, p.l2, p.dyadic);
+  const long long toff = TILE ? (long long)(a - p.inc_a0) * p.inc_as + (diag ? 0 : (long long)(b - p.inc_b0) * (p.l2 - 1)) : 0;
+  const float *__restrict__ itile = TILE ? p.inc + toff : nullptr;
+  float *__restrict__ gtile = TILE ? p.gt + toff : nullptr;
   const int nblk = lay.nblk;
   float *__restrict__ fr = p.fronts + pidx * lay.pair_floats;
   double *kbr = reinterpret_cast<double *>(fr + lay.kb_off);
@@ -146,47 +175,61 @@ __global__ __launch_bounds__(256) void pde_adj_kernel(PdeBwdArgs p) {
   // LDS: [wave] { coarse-row accumulators (IC x DP doubles) | dx (IC x DP floats) }
   double *gacc = ldsd + (size_t)wave * pde_lds_wave_doubles(IC, DP);
   float *dxs = reinterpret_cast<float *>(gacc + (size_t)IC * DP);
-  for (int r = lane; r < IC; r += 64) {
+  if constexpr (!TILE) {
+    for (int r = lane; r < IC; r += 64) {
 #pragma unroll
-    for (int k = 0; k < DP; ++k) {
-      dxs[r * DP + k] = k < d ? x[(r + 1) * d + k] - x[r * d + k] : 0.0f;
-      gacc[r * DP + k] = 0.0;
+      for (int k = 0; k < DP; ++k) {
+        dxs[r * DP + k] = k < d ? x[(r + 1) * d + k] - x[r * d + k] : 0.0f;
+        gacc[r * DP + k] = 0.0;
+      }
     }
   }
   __syncthreads();
 
   // the current column block: first fine column, lanes used, y increments of the lane's coarse columns
   int c0 = 0, U = 0;
-  float dy[WC][DP];
-  double dyd[WC][DP];  // fp64 copies for the contractions (converted once, not per cell)
+  float dy[WC][DPA];
+  double dyd[WC][DPA];  // fp64 copies for the contractions (converted once, not per cell)
   auto load_block = [&](int blk) {
     c0 = blk * CB;
     U = (J - c0 + W - 1) / W;
     U = U < 64 ? U : 64;
+    if constexpr (!TILE) {
 #pragma unroll
-    for (int w = 0; w < WC; ++w) {
-      int cj = c0 / REP + lane * WC + w;
-      cj = cj < JC - 1 ? cj : JC - 1;
+      for (int w = 0; w < WC; ++w) {
+        int cj = c0 / REP + lane * WC + w;
+        cj = cj < JC - 1 ? cj : JC - 1;
 #pragma unroll
-      for (int k = 0; k < DP; ++k) {
-        dy[w][k] = k < d ? y[(cj + 1) * d + k] - y[cj * d + k] : 0.0f;
-        dyd[w][k] = (double)dy[w][k];
+        for (int k = 0; k < DP; ++k) {
+          dy[w][k] = k < d ? y[(cj + 1) * d + k] - y[cj * d + k] : 0.0f;
+          dyd[w][k] = (double)dy[w][k];
+        }
       }
     }
   };
 
   const bool s1 = p.solver == 1;
   const bool hybrid = diag && p.solver == 0;
-  auto incs = [&](int ci, double (&inc)[WC], float (&dxv)[DP]) {
-    const float *dxr = dxs + ci * DP;
+  auto incs = [&](int ci, double (&inc)[WC], float (&dxv)[DPA]) {
+    if constexpr (TILE) {
 #pragma unroll
-    for (int k = 0; k < DP; ++k) dxv[k] = dxr[k];
+      for (int w = 0; w < WC; ++w) {
+        int cj = c0 / REP + lane * WC + w;
+        cj = cj < JC - 1 ? cj : JC - 1;
+        inc[w] = (double)tile_inc_b(itile, p.inc_ld, sub, ci, cj) * inv_factor;
+      }
+      dxv[0] = 0.0f;
+    } else {
+      const float *dxr = dxs + ci * DP;
 #pragma unroll
-    for (int w = 0; w < WC; ++w) {
-      float incf = 0.0f;
+      for (int k = 0; k < DP; ++k) dxv[k] = dxr[k];
 #pragma unroll
-      for (int k = 0; k < DP; ++k) incf = __builtin_fmaf(dxv[k], dy[w][k], incf);
-      inc[w] = (double)incf * inv_factor;
+      for (int w = 0; w < WC; ++w) {
+        float incf = 0.0f;
+#pragma unroll
+        for (int k = 0; k < DP; ++k) incf = __builtin_fmaf(dxv[k], dy[w][k], incf);
+        inc[w] = (double)incf * inv_factor;
+      }
     }
   };
 
@@ -214,7 +257,7 @@ __global__ __launch_bounds__(256) void pde_adj_kernel(PdeBwdArgs p) {
     const int ci = s - lane;
     if (ci >= 0 && ci < IC && lane < U) {
       double inc[WC], A[WC], B[WC];
-      float dxv[DP];
+      float dxv[DPA];
       incs(ci, inc, dxv);
 #pragma unroll
       for (int w = 0; w < WC; ++w) {
@@ -297,9 +340,12 @@ __global__ __launch_bounds__(256) void pde_adj_kernel(PdeBwdArgs p) {
     return;
   }
   const float g = diag ? p.gout[a] : p.gout[(long long)a * p.n2 + b];
+  // TILE: the coarse-cell sums scaled to dLoss/d<dx_i, dy_j> of the tile cell: 4^-n g (x2 for k(x, x)),
+  // and 4^-sub for the kernel cells a tile cell covers (inc = tile / 4^sub)
+  const double gts = TILE ? (diag ? 2.0 : 1.0) * inv_factor * (double)g / (double)(1 << (2 * sub)) : 0.0;
   // ---- pass B: blocks right to left, chunks backwards; the R sweep runs in its own step order
   double ru[W], rlast[REP], rcorner;
-  double gcol[WC][DP];
+  double gcol[WC][DPA];
   for (int blk = nblk - 1; ok && blk >= 0; --blk) {
     load_block(blk);
     kin = blk > 0 ? kbr + (long long)blk * (I + 1) : nullptr;
@@ -344,7 +390,7 @@ __global__ __launch_bounds__(256) void pde_adj_kernel(PdeBwdArgs p) {
         const int ci = s0 + h - lane;
         if (ci >= 0 && ci < IC && lane < U) {
           double inc[WC], S[WC];
-          float dxv[DP];
+          float dxv[DPA];
           incs(ci, inc, dxv);
 #pragma unroll
           for (int w = 0; w < WC; ++w) {
@@ -374,6 +420,20 @@ __global__ __launch_bounds__(256) void pde_adj_kernel(PdeBwdArgs p) {
 #pragma unroll
             for (int r = 0; r < REP; ++r) rout[ci * REP + r] = rlast[r];
           }
+          if constexpr (TILE) {
+            // the lane's coarse cells of row ci (columns of the sequence only); several kernel cells share a
+            // tile cell when sub > 0 (atomics), one writer otherwise
+#pragma unroll
+            for (int w = 0; w < WC; ++w) {
+              const int cj = c0 / REP + lane * WC + w;
+              if (cj < JC) {
+                float *gp = gtile + (long long)(ci >> sub) * p.inc_ld + (cj >> sub);
+                const float v = (float)(gts * S[w]);
+                if (sub) unsafeAtomicAdd(gp, v);
+                else *gp = v;
+              }
+            }
+          } else {
           double grow[DP], dxd[DP];
 #pragma unroll
           for (int k = 0; k < DP; ++k) {
@@ -390,11 +450,12 @@ __global__ __launch_bounds__(256) void pde_adj_kernel(PdeBwdArgs p) {
 #pragma unroll
           for (int k = 0; k < DP; ++k)
             if (k < d) atomicAdd(gacc + ci * DP + k, grow[k]);
+          }
         }
         rcorner = right[0];
       }
     }
-    if constexpr (COLS) {
+    if constexpr (COLS && !TILE) {
       if (!diag) {
         // columns: H[j] = 4^-n sum over coarse column j; dK/dy_j = H[j-1] - H[j]
         const double sy = inv_factor * (double)g;
@@ -416,6 +477,7 @@ __global__ __launch_bounds__(256) void pde_adj_kernel(PdeBwdArgs p) {
   }
   __syncthreads();  // the row accumulators are complete
   if (!ok) return;
+  if constexpr (TILE) return;  // the host contracts the tile with the increments
 
   // dK/dx_i = G[i-1] - G[i] with G[r] = 4^-n gacc[r] (x2 for k(x, x)), times the upstream gradient
   const double sx = (diag ? 2.0 : 1.0) * inv_factor * (double)g;
@@ -433,7 +495,7 @@ static int launch_pde_adj(const PdeBwdArgs &a, long long nblocks, hipStream_t s)
   if constexpr (W < REP || REP * W > 64) {
     return GPSIG_EUNSUPPORTED;
   } else {
-    const size_t lds = (size_t)a.wpb * pde_lds_wave_doubles(a.l1 - 1, DP) * sizeof(double);
+    const size_t lds = DP == 0 ? 0 : (size_t)a.wpb * pde_lds_wave_doubles(a.l1 - 1, DP) * sizeof(double);
     if (lds > 160 * 1024) return GPSIG_EUNSUPPORTED;
     // the column (dK/dy) accumulators only for cross pairs; k(x, x) takes twice the row part
     if (a.pair_mode == GPSIG_PAIRS_DIAG || MODE == 1)
@@ -458,9 +520,10 @@ static int pde_adj_w(const PdeBwdArgs &a, long long nblocks, int W, hipStream_t 
 
 template <int DP, int MODE>
 static int pde_adj_rep(const PdeBwdArgs &a, long long nblocks, hipStream_t s) {
-  const int rep = 1 << a.dyadic;
-  const int W = pde_bwd_cols(rep * (a.l2 - 1), rep);
-  switch (a.dyadic) {
+  const int kd = a.dyadic - (DP == 0 ? a.sub : 0);  // the kernel's refinement (TILE: past the tile's cells)
+  const int rep = 1 << kd;
+  const int W = pde_bwd_cols(rep * ((a.l2 - 1) << (DP == 0 ? a.sub : 0)), rep);
+  switch (kd) {
     case 0: return pde_adj_w<DP, 1, MODE>(a, nblocks, W, s);
     case 1: return pde_adj_w<DP, 2, MODE>(a, nblocks, W, s);
     case 2: return pde_adj_w<DP, 4, MODE>(a, nblocks, W, s);

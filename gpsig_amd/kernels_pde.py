@@ -12,9 +12,9 @@ Differences from the reference, deliberately not reproduced (SURVEY.md section 2
   * SignatureRBF/SignatureLinear pass ``order`` positionally into ``lengthscales``
     (kernels_pde.py:409,426); here ``order`` goes to ``order``;
   * the 1024-point cap of the CUDA op (kernels_pde.py:53) is gone for both implementations, as for the
-    reference's Cython path: the gfx950 solver sweeps long grids in column blocks (dyadic order <= 2;
-    bounded by the LDS for the boundary columns, about 4700 refined rows); the gradient keeps
-    2^order * (len-1) <= 1024 refined columns (GpsigError beyond).
+    reference's Cython path: the gfx950 solver and its adjoint sweep long grids in column blocks, and
+    channel counts past 16 or dyadic orders past 4 (adjoint: 3) run on increment tiles (the coarse
+    increment Gram as one matrix-core GEMM, the reference's own tf.matmul split, kernels_pde.py:176).
 """
 from __future__ import annotations
 
@@ -25,8 +25,6 @@ from . import autograd as _ag
 from . import lags as _lags
 from . import ops
 from .kernels import DEFAULT_JITTER, _as_tensor, _tensor_inner_product, _tensor_logs
-
-PDE_MAX_COLUMNS = 1024  # refined columns of the gradient kernel (gpsig_pde_vjp)
 
 
 class UntruncSignatureKernel:

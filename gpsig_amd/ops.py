@@ -46,6 +46,24 @@ def workspace(device, nbytes: int) -> torch.Tensor:
         return buf
 
 
+def scratch(device, nbytes: int):
+    """A second per-stream cached buffer for calls that take a workspace AND a scratch (the PDE adjoint's
+    fronts plus the increment tiles); None when nothing is needed."""
+    if nbytes <= 0:
+        return None
+    key = ("scratch", torch.device(device).index, torch.cuda.current_stream(device).cuda_stream)
+    with _ws_lock:
+        buf = _ws.get(key)
+        if buf is None or buf.numel() < nbytes:
+            buf = torch.empty(max(nbytes, 1 << 20), dtype=torch.uint8, device=device)
+            _ws[key] = buf
+        return buf
+
+
+def _sp(buf):
+    return (None, 0) if buf is None else (buf.data_ptr(), buf.numel())
+
+
 def release_workspaces() -> None:
     """Drop the cached per-stream scratch buffers (feature records, the PDE VJP's K_rev cells -- up to
     PDE_VJP_SCRATCH bytes); the next call allocates again.  Captured graphs (gpsig_amd.graphs) keep
@@ -270,7 +288,8 @@ def pde_diag(X: torch.Tensor, dyadic: int = 0, solver: int = 1) -> torch.Tensor:
     out = torch.empty((n,), dtype=torch.float32, device=X.device)
     if n == 0:
         return out
-    L.check(lib.gpsig_pde_diag(X.data_ptr(), n, l, d, dyadic, solver, out.data_ptr(), _stream(X.device)),
+    sp, sb = _sp(scratch(X.device, lib.gpsig_pde_scratch_bytes(n, l, n, l, d, dyadic, L.PAIRS_DIAG)))
+    L.check(lib.gpsig_pde_diag_ex(X.data_ptr(), n, l, d, dyadic, solver, out.data_ptr(), sp, sb, _stream(X.device)),
             "gpsig_pde_diag")
     return out
 
@@ -291,9 +310,10 @@ def pde_gram(X: torch.Tensor, Y: torch.Tensor | None = None, dyadic: int = 0, so
         out = torch.empty((r1 - out_row0, n2), dtype=torch.float32, device=X.device)
     if n1 == 0 or n2 == 0 or r1 == r0:
         return out
-    rc = lib.gpsig_pde_gram(X.data_ptr(), n1, l1, Y.data_ptr(), n2, l2, d, dyadic, solver,
-                            L.PAIRS_UPPER if sym else L.PAIRS_RECT, r0, r1, out.data_ptr(), out_row0, out.shape[-2],
-                            _stream(X.device))
+    pm = L.PAIRS_UPPER if sym else L.PAIRS_RECT
+    sp, sb = _sp(scratch(X.device, lib.gpsig_pde_scratch_bytes(n1, l1, n2, l2, d, dyadic, pm)))
+    rc = lib.gpsig_pde_gram_ex(X.data_ptr(), n1, l1, Y.data_ptr(), n2, l2, d, dyadic, solver, pm, r0, r1,
+                               out.data_ptr(), out_row0, out.shape[-2], sp, sb, _stream(X.device))
     L.check(rc, "gpsig_pde_gram")
     return out
 
@@ -312,11 +332,13 @@ def pde_diag_vjp(X: torch.Tensor, gout: torch.Tensor, dyadic: int = 0, solver: i
         gX = torch.zeros((n, l, d), dtype=torch.float32, device=X.device)
     per = lib.gpsig_pde_vjp_workspace_bytes(1, l, l, dyadic)
     step = max(1, min(n, PDE_VJP_SCRATCH // max(per, 1)))
+    sp, sb = _sp(scratch(X.device, lib.gpsig_pde_vjp_scratch_bytes(n, l, n, l, d, dyadic, L.PAIRS_DIAG)))
     for r0 in range(0, n, step):
         r1 = min(n, r0 + step)
         ws = workspace(X.device, lib.gpsig_pde_vjp_workspace_bytes(r1 - r0, l, l, dyadic))
-        rc = lib.gpsig_pde_vjp(X.data_ptr(), n, l, X.data_ptr(), n, l, d, dyadic, solver, L.PAIRS_DIAG, r0, r1,
-                               gout.data_ptr(), gX.data_ptr(), None, ws.data_ptr(), ws.numel(), _stream(X.device))
+        rc = lib.gpsig_pde_vjp_ex(X.data_ptr(), n, l, X.data_ptr(), n, l, d, dyadic, solver, L.PAIRS_DIAG, r0, r1,
+                                  gout.data_ptr(), gX.data_ptr(), None, ws.data_ptr(), ws.numel(), sp, sb,
+                                  _stream(X.device))
         L.check(rc, "gpsig_pde_vjp")
     return gX
 
@@ -336,12 +358,13 @@ def pde_gram_vjp(X: torch.Tensor, Y: torch.Tensor | None, gout: torch.Tensor, dy
     gY = gX if sym else torch.zeros((n2, l2, d), dtype=torch.float32, device=X.device)
     per = lib.gpsig_pde_vjp_workspace_bytes(n2, l1, l2, dyadic)
     step = max(4, (min(n1, PDE_VJP_SCRATCH // max(per, 1)) // 4) * 4)
+    sp, sb = _sp(scratch(X.device, lib.gpsig_pde_vjp_scratch_bytes(n1, l1, n2, l2, d, dyadic, L.PAIRS_RECT)))
     for r0 in range(0, n1, step):
         r1 = min(n1, r0 + step)
         ws = workspace(X.device, lib.gpsig_pde_vjp_workspace_bytes((r1 - r0) * n2, l1, l2, dyadic))
-        rc = lib.gpsig_pde_vjp(X.data_ptr(), n1, l1, Y.data_ptr(), n2, l2, d, dyadic, solver, L.PAIRS_RECT, r0, r1,
-                               gout.data_ptr(), gX.data_ptr(), gY.data_ptr(), ws.data_ptr(), ws.numel(),
-                               _stream(X.device))
+        rc = lib.gpsig_pde_vjp_ex(X.data_ptr(), n1, l1, Y.data_ptr(), n2, l2, d, dyadic, solver, L.PAIRS_RECT, r0,
+                                  r1, gout.data_ptr(), gX.data_ptr(), gY.data_ptr(), ws.data_ptr(), ws.numel(), sp, sb,
+                                  _stream(X.device))
         L.check(rc, "gpsig_pde_vjp")
     return gX, (None if sym else gY)
 
@@ -367,9 +390,10 @@ def pde_fronts(X: torch.Tensor, Y: torch.Tensor | None, dyadic: int, solver: int
     if fronts.dtype != torch.float32 or not fronts.is_contiguous() or fronts.numel() * 4 < pde_fronts_bytes(npairs, l1, l2, dyadic):
         raise ValueError("fronts must be a contiguous float32 buffer of pde_fronts_bytes() bytes")
     out = torch.empty((n1,) if diag else (n1, n2), dtype=torch.float32, device=X.device)
-    rc = lib.gpsig_pde_fronts(X.data_ptr(), n1, l1, Y.data_ptr(), n2, l2, d, dyadic, solver,
-                              L.PAIRS_DIAG if diag else L.PAIRS_RECT, 0, n1, out.data_ptr(), fronts.data_ptr(),
-                              fronts.numel() * 4, _stream(X.device))
+    pm = L.PAIRS_DIAG if diag else L.PAIRS_RECT
+    sp, sb = _sp(scratch(X.device, lib.gpsig_pde_vjp_scratch_bytes(n1, l1, n2, l2, d, dyadic, pm)))
+    rc = lib.gpsig_pde_fronts_ex(X.data_ptr(), n1, l1, Y.data_ptr(), n2, l2, d, dyadic, solver, pm, 0, n1,
+                                 out.data_ptr(), fronts.data_ptr(), fronts.numel() * 4, sp, sb, _stream(X.device))
     L.check(rc, "gpsig_pde_fronts")
     if sym and not diag:  # k(x_a, x_b) = k(x_b, x_a): the upper triangle mirrored, as pde_gram's
         out = torch.triu(out) + torch.triu(out, 1).T
@@ -389,10 +413,11 @@ def pde_vjp_fronts(X: torch.Tensor, Y: torch.Tensor | None, gout: torch.Tensor, 
     n2, l2, _ = Y.shape
     gX = torch.zeros((n1, l1, d), dtype=torch.float32, device=X.device)
     gY = gX if (sym or diag) else torch.zeros((n2, l2, d), dtype=torch.float32, device=X.device)
-    rc = lib.gpsig_pde_vjp_fronts(X.data_ptr(), n1, l1, Y.data_ptr(), n2, l2, d, dyadic, solver,
-                                  L.PAIRS_DIAG if diag else L.PAIRS_RECT, 0, n1, gout.data_ptr(), gX.data_ptr(),
-                                  None if diag else gY.data_ptr(), fronts.data_ptr(), fronts.numel() * 4,
-                                  _stream(X.device))
+    pm = L.PAIRS_DIAG if diag else L.PAIRS_RECT
+    sp, sb = _sp(scratch(X.device, lib.gpsig_pde_vjp_scratch_bytes(n1, l1, n2, l2, d, dyadic, pm)))
+    rc = lib.gpsig_pde_vjp_fronts_ex(X.data_ptr(), n1, l1, Y.data_ptr(), n2, l2, d, dyadic, solver, pm, 0, n1,
+                                     gout.data_ptr(), gX.data_ptr(), None if diag else gY.data_ptr(),
+                                     fronts.data_ptr(), fronts.numel() * 4, sp, sb, _stream(X.device))
     L.check(rc, "gpsig_pde_vjp_fronts")
     if diag:
         return gX

@@ -221,6 +221,18 @@ int gpsig_pde_gram(const float *X, int n1, int l1, const float *Y, int n2, int l
 
 int gpsig_pde_diag(const float *X, int n, int l, int d, int dyadic, int solver, float *out, gpsig_stream_t stream);
 
+/* Channel counts past 16 and dyadic orders past 4 run the solver on increment tiles: the coarse increment Gram
+ * <dx_i, dy_j> of a chunk of pairs is one matrix-core GEMM (the reference's own split, kernels_pde.py:176
+ * tf.matmul before the op), the solver reads it; any channel count, dyadic <= 8.  Those calls need a scratch
+ * of gpsig_pde_scratch_bytes(...) bytes (0 otherwise; the entries above pass none and return
+ * GPSIG_EWORKSPACE there). */
+size_t gpsig_pde_scratch_bytes(int n1, int l1, int n2, int l2, int d, int dyadic, int pair_mode);
+int gpsig_pde_gram_ex(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int dyadic, int solver,
+                      int pair_mode, int row_begin, int row_end, float *out, int out_row0, int out_rows, void *scratch,
+                      size_t scratch_bytes, gpsig_stream_t stream);
+int gpsig_pde_diag_ex(const float *X, int n, int l, int d, int dyadic, int solver, float *out, void *scratch,
+                      size_t scratch_bytes, gpsig_stream_t stream);
+
 /* Gradient of gpsig_pde_gram / gpsig_pde_diag: the reference's own adjoint (kernels_pde.py:465-509,
  * _KdiagGrad; covariance_op/_untrunc_cov_grad.py:25-77): KK = K (.) flip(K_rev) with K_rev solved on the
  * time-reversed paths by the first-order scheme, contracted with the increments.  pair_mode DIAG
@@ -229,8 +241,9 @@ int gpsig_pde_diag(const float *X, int n, int l, int d, int dyadic, int solver, 
  * is re-solved on the mirrored wavefront and meets the forward sweep lane by lane; the workspace holds
  * the forward sweep's fronts (fp32, every few coarse steps, about (1 + REP/W) I J / H floats per pair;
  * I = 2^dyadic (l1-1), J = 2^dyadic (l2-1)), gpsig_pde_vjp_workspace_bytes(pairs, l1, l2, dyadic), which
- * returns 0 where the kernel does not apply (dyadic > 3: GPSIG_EUNSUPPORTED).  Wider grids than one
- * wave's 64 W columns are swept in column blocks; their fp64 boundary columns are part of the workspace. */
+ * returns 0 where the kernel does not apply.  Wider grids than one wave's 64 W columns are swept in column
+ * blocks; their fp64 boundary columns are part of the workspace.  Past dyadic 3 (and past 16 channels) the
+ * _ex entries below apply (the fronts then follow the grid refined 2^(dyadic - 3) per tile cell). */
 size_t gpsig_pde_vjp_workspace_bytes(int npairs, int l1, int l2, int dyadic);
 
 int gpsig_pde_vjp(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int dyadic, int solver,
@@ -249,6 +262,23 @@ int gpsig_pde_fronts(const float *X, int n1, int l1, const float *Y, int n2, int
 int gpsig_pde_vjp_fronts(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int dyadic,
                          int solver, int pair_mode, int row_begin, int row_end, const float *gout, float *gX,
                          float *gY, const void *fronts, size_t fronts_bytes, gpsig_stream_t stream);
+
+/* The adjoint entries with the scratch of the increment-tile path (d > 16 or dyadic > 3: the increment
+ * tile, the adjoint's coarse-cell sums as dLoss/d<dx_i, dy_j> in a tile of the same layout, contracted with
+ * the increments by two matrix-core GEMMs); gpsig_pde_vjp_scratch_bytes(...) bytes, 0 where the fixed
+ * kernels apply. */
+size_t gpsig_pde_vjp_scratch_bytes(int n1, int l1, int n2, int l2, int d, int dyadic, int pair_mode);
+int gpsig_pde_vjp_ex(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int dyadic, int solver,
+                     int pair_mode, int row_begin, int row_end, const float *gout, float *gX, float *gY,
+                     void *workspace, size_t workspace_bytes, void *scratch, size_t scratch_bytes,
+                     gpsig_stream_t stream);
+int gpsig_pde_fronts_ex(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int dyadic, int solver,
+                        int pair_mode, int row_begin, int row_end, float *out, void *fronts, size_t fronts_bytes,
+                        void *scratch, size_t scratch_bytes, gpsig_stream_t stream);
+int gpsig_pde_vjp_fronts_ex(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int dyadic,
+                            int solver, int pair_mode, int row_begin, int row_end, const float *gout, float *gX,
+                            float *gY, const void *fronts, size_t fronts_bytes, void *scratch, size_t scratch_bytes,
+                            gpsig_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Truncated signatures (replaces iisignature.sig behind iisignature_tensorflow.Sig,

@@ -36,6 +36,7 @@ def _load():
         _lib.sigpde_gram.argtypes = [dp, i, i, dp, i, i, i, i, i, i, dp]
         _lib.sigpde_diag.argtypes = [dp, i, i, i, i, i, dp]
         _lib.sigpde_diag_grids.argtypes = [dp, i, i, i, i, i, dp, dp]
+        _lib.sigpde_gram_grad.argtypes = [dp, i, i, dp, i, i, i, i, i, dp, dp, dp]
     return _lib
 
 
@@ -73,3 +74,16 @@ def pde_diag_grids(X, dyadic=0, solver=1):
     Kr = np.zeros((A, G, G))
     lib.sigpde_diag_grids(_p(X), A, L, D, dyadic, solver, _p(K), _p(Kr))
     return K, Kr
+
+
+def pde_gram_grad(X, Y, W, dyadic=0, solver=1):
+    """sum_ab W[a, b] (dK(x_a, y_b)/dX, dK/dY) by the reference's adjoint (oracle/pde_grad.py pair_grad, in C):
+    X (n1,l1,d), Y (n2,l2,d), W (n1,n2) -> (gX, gY)."""
+    lib = _load()
+    X = np.ascontiguousarray(X, dtype=np.float64)
+    Y = np.ascontiguousarray(Y, dtype=np.float64)
+    W = np.ascontiguousarray(W, dtype=np.float64)
+    gX, gY = np.zeros_like(X), np.zeros_like(Y)
+    lib.sigpde_gram_grad(_p(X), X.shape[0], X.shape[1], _p(Y), Y.shape[0], Y.shape[1], X.shape[2], dyadic, solver,
+                         _p(W), _p(gX), _p(gY))
+    return gX, gY

@@ -106,3 +106,58 @@ void sigpde_diag_grids(const double *X, int A, int L, int d, int n, int solver, 
     sigpde_pair(x, L, x, L, d, n, 0, 1, 0, Krev + (size_t)a * G * G);
   }
 }
+
+/* The reference's adjoint (kernels_pde.py:465-509 restated in oracle/pde_grad.py pair_grad) for one cross
+ * pair: KK[i][j] = K[i][j] K_rev[I-1-i][J-1-j] (K_rev: solver 0 on the reversed paths), coarse-row / column
+ * sums contracted with the other path's increments, / 4^n; gx[p] = Gx[p-1] - Gx[p], gy likewise. */
+void sigpde_pair_grad(const double *x, int lx, const double *y, int ly, int d, int n, int solver, double *gx,
+                      double *gy) {
+  const int rep = 1 << n;
+  const int I = rep * (lx - 1), J = rep * (ly - 1);
+  double *K = (double *)malloc(sizeof(double) * (size_t)(I + 1) * (J + 1));
+  double *Kr = (double *)malloc(sizeof(double) * (size_t)(I + 1) * (J + 1));
+  double *Gx = (double *)calloc((size_t)(lx - 1) * d, sizeof(double));
+  double *Gy = (double *)calloc((size_t)(ly - 1) * d, sizeof(double));
+  sigpde_pair(x, lx, y, ly, d, n, solver, 0, 0, K);
+  sigpde_pair(x, lx, y, ly, d, n, 0, 1, 0, Kr);
+  for (int i = 0; i < I; ++i)
+    for (int j = 0; j < J; ++j) {
+      const double kk = K[(size_t)i * (J + 1) + j] * Kr[(size_t)(I - 1 - i) * (J + 1) + (J - 1 - j)];
+      const int ii = i >> n, jj = j >> n;
+      for (int k = 0; k < d; ++k) {
+        Gx[(size_t)ii * d + k] += kk * (y[(jj + 1) * d + k] - y[jj * d + k]);
+        Gy[(size_t)jj * d + k] += kk * (x[(ii + 1) * d + k] - x[ii * d + k]);
+      }
+    }
+  const double f = 1.0 / (double)(1 << (2 * n));
+  for (int p = 0; p < lx; ++p)
+    for (int k = 0; k < d; ++k)
+      gx[(size_t)p * d + k] = f * ((p > 0 ? Gx[(size_t)(p - 1) * d + k] : 0.0) - (p < lx - 1 ? Gx[(size_t)p * d + k] : 0.0));
+  for (int p = 0; p < ly; ++p)
+    for (int k = 0; k < d; ++k)
+      gy[(size_t)p * d + k] = f * ((p > 0 ? Gy[(size_t)(p - 1) * d + k] : 0.0) - (p < ly - 1 ? Gy[(size_t)p * d + k] : 0.0));
+  free(K);
+  free(Kr);
+  free(Gx);
+  free(Gy);
+}
+
+/* sum over pairs of w[a][b] * (dK(x_a, y_b)/dX, dK/dY), pairs in parallel (per-pair buffers, summed in order) */
+void sigpde_gram_grad(const double *X, int n1, int l1, const double *Y, int n2, int l2, int d, int n, int solver,
+                      const double *w, double *gX, double *gY) {
+  double *px = (double *)calloc((size_t)n1 * n2 * l1 * d, sizeof(double));
+  double *py = (double *)calloc((size_t)n1 * n2 * l2 * d, sizeof(double));
+#pragma omp parallel for schedule(dynamic, 1)
+  for (long t = 0; t < (long)n1 * n2; ++t) {
+    const int a = (int)(t / n2), b = (int)(t % n2);
+    sigpde_pair_grad(X + (size_t)a * l1 * d, l1, Y + (size_t)b * l2 * d, l2, d, n, solver, px + (size_t)t * l1 * d,
+                     py + (size_t)t * l2 * d);
+  }
+  for (long t = 0; t < (long)n1 * n2; ++t) {
+    const int a = (int)(t / n2), b = (int)(t % n2);
+    for (long e = 0; e < (long)l1 * d; ++e) gX[(size_t)a * l1 * d + e] += w[t] * px[(size_t)t * l1 * d + e];
+    for (long e = 0; e < (long)l2 * d; ++e) gY[(size_t)b * l2 * d + e] += w[t] * py[(size_t)t * l2 * d + e];
+  }
+  free(px);
+  free(py);
+}

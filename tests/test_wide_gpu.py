@@ -179,3 +179,94 @@ def test_wide_vjp_other_seeds(base, difference):
     (ar.k_seq(Xr, Yr, M, base, difference=difference) * torch.tensor(G)).sum().backward()
     assert norm_rel_err(gX.cpu().numpy(), Xr.grad.numpy()) < GTOL
     assert norm_rel_err(gY.cpu().numpy(), Yr.grad.numpy()) < GTOL
+
+
+# ----------------------------------------------------------------------------- inducing tensors
+@pytest.mark.parametrize("D,L", [(46, 136), (126, 136), (46, 500)])
+@pytest.mark.parametrize("increments", [False, True])
+def test_wide_tens_vs_seq(D, L, increments):
+    """K_tens_vs_seq raw levels (the wide port of the packed recursion) vs the oracle at the runners'
+    channel counts (InducingTensors with increments=True is what train_gpsig.py trains)."""
+    from gpsig_amd import ops
+    M, T, N = 4, 5, 70
+    LT = M * (M + 1) // 2
+    rng = np.random.default_rng(D + L + increments)
+    Z = rng.standard_normal((LT, T, 2, D) if increments else (LT, T, D)) * (2.0 / np.sqrt(D))
+    X = walks(rng, N, L, D, 2.0)
+    ref = kr.SignatureKernelRef(L * D, D, M, normalization=False)
+    exp = ref.K_tens_vs_seq_raw(Z, X, increments=increments)
+    got = ops.tens_vs_seq(t(Z), t(X), M, increments=increments).cpu().numpy()
+    assert (norm_rel_err(got[1:], exp[1:], axis_levels=True) < TOL).all()
+
+
+@pytest.mark.parametrize("order,difference,base", [(2, True, "rbf"), (1, False, "rbf"), (1, True, "linear"),
+                                                   (3, True, "linear")])
+def test_wide_tens_vs_seq_generic(order, difference, base):
+    """The generic kernel (orders > 1, difference=False) and the linear seed at a wide channel count."""
+    from gpsig_amd import ops
+    M, T, N, D, L = 3, 4, 20, 40, 18
+    LT = M * (M + 1) // 2
+    rng = np.random.default_rng(order * 10 + difference)
+    Z = rng.standard_normal((LT, T, 2, D)) * (2.0 / np.sqrt(D))
+    X = walks(rng, N, L, D, 2.0)
+    ref = kr.SignatureKernelRef(L * D, D, M, normalization=False, order=order, difference=difference, base=base)
+    exp = ref.K_tens_vs_seq_raw(Z, X, increments=True)
+    got = ops.tens_vs_seq(t(Z), t(X), M, order=order, base=base, difference=difference, increments=True).cpu().numpy()
+    assert (norm_rel_err(got[1:], exp[1:], axis_levels=True) < TOL).all()
+
+
+@pytest.mark.parametrize("increments", [False, True])
+def test_wide_tens_gram(increments):
+    from gpsig_amd import ops
+    M, T, D = 4, 37, 46
+    LT = M * (M + 1) // 2
+    rng = np.random.default_rng(3 + increments)
+    Z = rng.standard_normal((LT, T, 2, D) if increments else (LT, T, D)) * (2.0 / np.sqrt(D))
+    exp = kr.SignatureKernelRef(4 * D, D, M).K_tens_raw(Z, increments=increments)
+    got = ops.tens_gram(t(Z), M, increments=increments).cpu().numpy()
+    assert (norm_rel_err(got[1:], exp[1:], axis_levels=True) < TOL).all()
+
+
+@pytest.mark.parametrize("D,L", [(46, 136), (126, 40), (46, 500)])
+@pytest.mark.parametrize("base", ["rbf", "linear"])
+@pytest.mark.parametrize("increments", [True, False])
+def test_wide_tens_vs_seq_vjp(D, L, base, increments):
+    """Kuf gradients (point-weight tiles + the emission GEMMs) vs fp64 autodiff, normalised K_tens_vs_seq,
+    with and without the forward's saved end state."""
+    import gpsig_amd
+    from oracle import autodiff_ref as ar
+    M, T, N = 3, 3, 67
+    LT = M * (M + 1) // 2
+    rng = np.random.default_rng(D + L)
+    Z = rng.standard_normal((LT, T, 2, D) if increments else (LT, T, D)) * (2.0 / np.sqrt(D))
+    X = walks(rng, N, L, D, 2.0)
+    G = rng.standard_normal((T, N))
+    cls = gpsig_amd.SignatureRBF if base == "rbf" else gpsig_amd.SignatureLinear
+    k = cls(L * D, D, M)
+    Zt = torch.tensor(Z, device=DEV, requires_grad=True)
+    Xt = torch.tensor(X.reshape(N, -1), device=DEV, requires_grad=True)
+    (k.K_tens_vs_seq(Zt, Xt, increments=increments) * torch.as_tensor(G, device=DEV)).sum().backward()
+    Zr, Xr = torch.tensor(Z, requires_grad=True), torch.tensor(X, requires_grad=True)
+    (ar.K_tens_vs_seq(Zr, Xr, M, base=base, increments=increments) * torch.tensor(G)).sum().backward()
+    assert norm_rel_err(Zt.grad.cpu().numpy(), Zr.grad.numpy()) < GTOL
+    assert norm_rel_err(Xt.grad.reshape(X.shape).cpu().numpy(), Xr.grad.numpy()) < GTOL
+
+
+@pytest.mark.parametrize("embedding", ["linear", "rbf"])
+def test_wide_rescaled(embedding):
+    """VOSF <S(x), (I - Lambda) S(x)> per level (signature_algs_vosf.py:11-48) at a wide channel count."""
+    from gpsig_amd import ops
+    M, T, N, D, L = 3, 4, 6, 30, 20
+    LT = M * (M + 1) // 2
+    rng = np.random.default_rng(5)
+    Z = rng.uniform(0.0, 1.0, (LT, T, D))
+    X = walks(rng, N, L, D, 2.0)
+    if embedding == "linear":
+        exp = kr.SignatureKernelRef(L * D, D, M, base="linear", normalization=False).mahalanobis_raw(Z, X)
+    else:  # per-coordinate RBF embedding (kernels_pde.py:191-222), as tests/golden/make_golden.py F5
+        from oracle import sigalgs
+        Zc = np.concatenate([Z, np.ones_like(Z)], axis=1)
+        E = np.exp(-(X[:, :, None, :] - X[:, None, :, :]) ** 2 / 2.0)
+        exp = sigalgs.signature_kern_rescaled_higher_order(np.einsum("npqd,rtd->nprtq", E, Zc), M)
+    got = ops.rescaled(t(Z), t(X), M, embedding=embedding).cpu().numpy()
+    assert (norm_rel_err(got[1:], exp[1:], axis_levels=True) < TOL).all()
