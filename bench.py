@@ -16,7 +16,6 @@ from __future__ import annotations
 
 import argparse
 import json
-import math
 import multiprocessing as mp
 import os
 import sys
@@ -62,6 +61,39 @@ def _cpu_worker(args):
     return done, time.perf_counter() - t0
 
 
+def _check_worker(args):
+    """Raw per-level Gram blocks (levels, a1-a0, b1-b0) of the float64 oracle for one block pair, and
+    the raw per-level diagonal of the rows of block a when it is a diagonal block."""
+    Xs, (a0, a1, b0, b1), l, d, m = args
+    os.environ["OMP_NUM_THREADS"] = "1"
+    from oracle import kernels_ref as kr  # checker only
+    k = kr.SignatureKernelRef(l * d, d, m, normalization=False)
+    blk = k.K_seq(Xs[a0:a1], Xs[b0:b1])
+    diag = k.K_seq_diag(Xs[a0:a1]) if a0 == b0 else None
+    return (a0, a1, b0, b1), blk, diag
+
+
+def oracle_subsample(Xnp, S, l, d, m, jitter, procs, blk=16):
+    """SURVEY.md 8d parity sample: the normalised K of the sequences S (the restriction of the normalised
+    Gram to S equals K(X[S]) -- normalisation is per sequence), the float64 oracle evaluated in blk x blk
+    block pairs (upper triangle) over a process pool, normalised as kernels.py:402-477 with the jitter."""
+    Xs = Xnp[S].astype(np.float64)
+    ns = len(S)
+    jobs = [(Xs, (a, min(a + blk, ns), b, min(b + blk, ns)), l, d, m)
+            for a in range(0, ns, blk) for b in range(a, ns, blk)]
+    raw = np.zeros((m + 1, ns, ns))
+    dg = np.zeros((m + 1, ns))
+    with mp.get_context("spawn").Pool(procs) as pool:
+        for (a0, a1, b0, b1), blkv, diag in pool.imap_unordered(_check_worker, jobs):
+            raw[:, a0:a1, b0:b1] = blkv
+            raw[:, b0:b1, a0:a1] = blkv.transpose(0, 2, 1)
+            if diag is not None:
+                dg[:, a0:a1] = diag
+    ds = np.sqrt(dg + jitter)
+    K = (raw + jitter * np.eye(ns)[None]) / (ds[:, :, None] * ds[:, None, :])
+    return K.sum(0)
+
+
 def _cpu_model():
     try:
         with open("/proc/cpuinfo") as f:
@@ -73,16 +105,20 @@ def _cpu_model():
     return "unknown"
 
 
-def cpu_baseline(l, d, m, seconds=15.0, n_blk=8):
-    """The fp64 NumPy restatement of the reference dataflow, one single-threaded process per core.
-    Cores: every CPU in the affinity mask, capped at the CPU share the job is given (OMP_NUM_THREADS,
-    16 on the GPU boxes, whose affinity mask shows the whole host)."""
+def cpu_procs():
+    """Every CPU in the affinity mask, capped at the CPU share the job is given (OMP_NUM_THREADS, 16 on
+    the GPU boxes, whose affinity mask shows the whole host)."""
     try:
         affinity = len(os.sched_getaffinity(0))
     except AttributeError:  # pragma: no cover
         affinity = os.cpu_count() or 1
     share = int(os.environ.get("OMP_NUM_THREADS", affinity) or affinity)
-    procs = max(1, min(affinity, share))
+    return max(1, min(affinity, share)), affinity
+
+
+def cpu_baseline(l, d, m, seconds=15.0, n_blk=8):
+    """The fp64 NumPy restatement of the reference dataflow, one single-threaded process per core."""
+    procs, affinity = cpu_procs()
     with mp.get_context("spawn").Pool(procs) as pool:
         res = pool.map(_cpu_worker, [(seconds, n_blk, l, d, m, 100 + i) for i in range(procs)])
     entries = sum(r[0] for r in res)
@@ -135,6 +171,8 @@ def main():
                     help="process-group backend (nccl = RCCL; gloo only to rehearse N>1 ranks on one GPU)")
     ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r2_gram_counters.json"),
                     help="per-launch HBM bytes of the Gram kernel from a PMC pass (profiles/*.json)")
+    ap.add_argument("--check-rows", type=int, default=256,
+                    help="rows of the max_abs_err subsample (SURVEY.md 8d: 256 for large N)")
     args = ap.parse_args()
 
     import torch
@@ -143,6 +181,9 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world} (launch N > 1 with "
+                         f"torch.distributed.run --nproc-per-node N)")
     dev = torch.device("cuda", local_rank % max(1, torch.cuda.device_count()))
     torch.cuda.set_device(dev)
     if world > 1:
@@ -150,6 +191,7 @@ def main():
             dist.init_process_group("nccl", device_id=dev)
         else:
             dist.init_process_group(args.backend)
+        assert dist.get_world_size() == args.gpus, (dist.get_world_size(), args.gpus)
 
     import gpsig_amd
     from gpsig_amd import _lib as L
@@ -179,6 +221,22 @@ def main():
         rows_done[0] += (a1 - a0) * n - (a1 * (a1 - 1) - a0 * (a0 - 1)) // 2
         return r
 
+    # HIP events around the collective and the mirror assembly (N > 1), on the current stream
+    phases = {"all_gather": [], "assemble": []}
+
+    class phase:
+        def __init__(self, name):
+            self.name = name
+
+        def __enter__(self):
+            self.e0 = torch.cuda.Event(enable_timing=True)
+            self.e0.record()
+
+        def __exit__(self, *exc):
+            e1 = torch.cuda.Event(enable_timing=True)
+            e1.record()
+            phases[self.name].append((self.e0, e1))
+
     gram_base = (L.BASE_RBF | (L.BASE_SEED_MFMA if args.seed_engine == "mfma" else 0)
                  | (L.GRAM_SPLIT if args.gram_path == "split" else 0))
 
@@ -187,12 +245,14 @@ def main():
         rs = kern._rsqrt_diag(Xs)
         return gdist.sharded_sym_gram(Xs, m, out_mode=L.OUT_NORM_SUM, compute=timed_compute, rs1=rs, rs2=rs,
                                       scale=kern._scale_vec(dev), jitter=kern.jitter, order=kern.order,
-                                      base=gram_base, difference=kern.difference)
+                                      base=gram_base, difference=kern.difference, phase=phase)
 
     for _ in range(args.warmup):
         K = step()
     torch.cuda.synchronize()
     ev.clear()
+    for v in phases.values():
+        v.clear()
     rows_done[0] = 0
     if world > 1:
         dist.barrier()
@@ -254,15 +314,35 @@ def main():
                      # algorithmic bytes the fused kernel never moves, so a ratio to a copy is meaningless.
                      "peak_probe": probe},
     }
+    # per-rank breakdown of a step (ms): the Gram launches, the all-gather and the mirror assembly
+    per_step = lambda evs: sum(a.elapsed_time(b) for a, b in evs) / args.steps  # noqa: E731
+    mine = {"rank": rank, "gram_ms": per_step(ev), "gram_launches": len(ev) // max(args.steps, 1),
+            "all_gather_ms": per_step(phases["all_gather"]), "assemble_ms": per_step(phases["assemble"]),
+            "step_ms": elapsed / args.steps * 1e3}
+    if world > 1:
+        ranks = [None] * world
+        dist.all_gather_object(ranks, mine)
+        backend = dist.get_backend()
+        lib = None
+        if backend == "nccl":
+            v = torch.cuda.nccl.version()
+            lib = "RCCL " + (".".join(map(str, v)) if isinstance(v, tuple) else str(v))
+        out["distributed"] = {"backend": backend, "collective_library": lib, "world_size": world,
+                              "per_rank": ranks,
+                              # all_gather_into_tensor output: world x 2 chunk slots x B rows x N fp32
+                              "gathered_bytes": world * 2 * gdist.triangle_chunks(n, world)[1] * n * 4}
+    else:
+        out["breakdown"] = mine
     if rank == 0 and not args.no_check:
-        # parity on a bounded subsample: the normalised Gram restricted to a subset S of the sequences
-        # equals K(X[S]) (per-sequence diagonals), which the float64 oracle evaluates directly
-        from oracle import kernels_ref as kr
-        S = np.unique(np.linspace(0, n - 1, 40).astype(int))
-        Kref = kr.SignatureKernelRef(l * d, d, m).K(Xnp[S].astype(np.float64).reshape(len(S), -1))
-        got = K[torch.as_tensor(S, device=dev)][:, torch.as_tensor(S, device=dev)].double().cpu().numpy()
+        # parity on a bounded subsample (256 rows): the normalised Gram restricted to a subset
+        # S of the sequences equals K(X[S]) (per-sequence diagonals), evaluated by the float64 oracle
+        S = np.unique(np.linspace(0, n - 1, min(n, args.check_rows)).astype(int))
+        Kref = oracle_subsample(Xnp, S, l, d, m, kern.jitter, cpu_procs()[0])
+        Si = torch.as_tensor(S, device=dev)
+        got = K[Si][:, Si].double().cpu().numpy()
         out["max_abs_err"] = float(np.abs(got - Kref).max())
         out["max_abs_ref"] = float(np.abs(Kref).max())
+        out["check_rows"] = len(S)
     if rank == 0 and world == 1 and not args.no_cpu:
         out["cpu_baseline"] = cpu_baseline(l, d, m, seconds=args.cpu_seconds)
     if rank == 0:

@@ -19,6 +19,7 @@ logic on CPU with the gloo backend (tests/test_distributed.py); the product path
 """
 from __future__ import annotations
 
+import contextlib
 import math
 
 import torch
@@ -97,13 +98,20 @@ def sym_from_gathered(gathered: torch.Tensor, n: int, world: int, levels: int, a
     return assemble(gathered, row_off, B * n, n, levels)
 
 
+def _no_phase(name):
+    return contextlib.nullcontext()
+
+
 def sharded_sym_gram(X: torch.Tensor, num_levels: int, *, out_mode: int = L.OUT_NORM_SUM, group=None,
-                     compute=None, assemble=None, **kw) -> torch.Tensor:
+                     compute=None, assemble=None, phase=None, **kw) -> torch.Tensor:
     """Full symmetric Gram on every rank.  kw: order, base, difference, rs1/rs2, scale, jitter.
+    phase(name) -> context manager around the "all_gather" and "assemble" steps (bench.py times them
+    with HIP events; the Gram launches are timed through `compute`).
 
     Returns (n, n) for OUT_NORM_SUM, else (num_levels+1, n, n).
     """
     compute = compute or _hip_compute
+    phase = phase or _no_phase
     rank, world = _world(group)
     n = X.shape[0]
     levels = 1 if out_mode == L.OUT_NORM_SUM else num_levels + 1
@@ -113,8 +121,10 @@ def sharded_sym_gram(X: torch.Tensor, num_levels: int, *, out_mode: int = L.OUT_
         return out[0] if out_mode == L.OUT_NORM_SUM else out
     local = sym_local_blocks(X, num_levels, rank, world, out_mode=out_mode, compute=compute, **kw)
     gathered = torch.empty((world * local.numel() // n, n), dtype=torch.float32, device=X.device)
-    dist.all_gather_into_tensor(gathered, local.reshape(-1, n), group=group)
-    full = sym_from_gathered(gathered, n, world, levels, assemble)
+    with phase("all_gather"):
+        dist.all_gather_into_tensor(gathered, local.reshape(-1, n), group=group)
+    with phase("assemble"):
+        full = sym_from_gathered(gathered, n, world, levels, assemble)
     return full[0] if out_mode == L.OUT_NORM_SUM else full
 
 
