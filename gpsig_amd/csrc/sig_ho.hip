@@ -10,6 +10,10 @@
 //   R'[a'][b'] = dM / ((a'+1)(b'+1)) * R[a'-1][b'-1]                        (:69, same cell)
 // so the state per column is the current row's blocks plus the running column sums
 // CB_m[b] = sum_{i'<i} sum_a R_m[a][b]; K_m = sum_j sum_b CB_m[b] at the end.
+// Sequences longer than the wave's 64 W columns run in column blocks of 64 W - 1 cells (the last
+// column is the halo point), left to right over all rows; the exclusive column scans of a block add the
+// carry of the blocks to its left: per row, one float per scanned quantity (S00 and Sa[1..dn-1] of each
+// level), kept in this wave's LDS slab.
 #include "sig_common.h"
 
 namespace gpsig {
@@ -23,16 +27,36 @@ struct HoLayout {
     return o;
   }
   static constexpr int total = off(MMAX + 1);
+  // column-block carries: the level-m scans of a row (S00 and Sa[1 .. dm(m+1)-1]) start at coff(m)
+  static constexpr int coff(int m) {
+    int o = 0;
+    for (int k = 1; k < m; ++k) o += dm(k + 1);
+    return o;
+  }
 };
+// scanned floats per row of a launch at num_levels M (the row stride of the carry slab)
+__host__ __device__ inline int ho_carries(int order, int M) {
+  int o = 0;
+  for (int k = 1; k < M; ++k) o += (k + 1 < order ? k + 1 : order);
+  return o;
+}
 
+// exclusive scan over the wave's columns; blocked launches (nblk > 1) add the carry cr of the blocks to
+// the left (written by lane 0 of the previous block) and leave the running total for the next one
 template <int W>
-GPSIG_DEV void excl_scan_cols(const float (&v)[W], float (&out)[W]) {
+GPSIG_DEV void excl_scan_cols(const float (&v)[W], float (&out)[W], float *cr, int blk, int nblk) {
   float t[W];
   t[0] = v[0];
 #pragma unroll
   for (int w = 1; w < W; ++w) t[w] = t[w - 1] + v[w];
   const float incl = group_incl_scan<64>(t[W - 1]);
-  const float base = incl - t[W - 1];
+  float base = incl - t[W - 1];
+  if (nblk > 1) {  // wave-uniform
+    const float cin = blk > 0 ? *cr : 0.0f;
+    const float tot = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, incl), 63));
+    if (blk + 1 < nblk && (threadIdx.x & 63) == 0) *cr = cin + tot;
+    base += cin;
+  }
   out[0] = base;
 #pragma unroll
   for (int w = 1; w < W; ++w) out[w] = base + t[w - 1];
@@ -71,8 +95,22 @@ __global__ __launch_bounds__(256) void sig_ho_kernel(SigArgs p) {
 
   const float *__restrict__ fx = p.FX + (long long)a * p.l1 * FS;
   const float *__restrict__ fy = p.FY + (long long)b * p.l2 * FS;
+  const int M = p.M;
+  const int nrows = Seed::DIFF ? p.l1 - 1 : p.l1;
+  constexpr int CPB = 64 * W - 1;
+  const int nblk = p.nblk;
+  const int ncar = ho_carries(ORD, M);
+  extern __shared__ float ho_carry[];
+  float *__restrict__ carry = ho_carry + (long long)wave * nrows * ncar;
+
+  float Kacc[MMAX + 1];
+#pragma unroll
+  for (int m = 0; m <= MMAX; ++m) Kacc[m] = 0.0f;
+
+  for (int blk = 0; blk < nblk; ++blk) {
+  const int j0 = blk * CPB;
   Seed seed;
-  seed.init(fx, fy, lane, p.l2);
+  seed.init(fx, fy + (long long)j0 * FS, lane, nblk == 1 ? p.l2 : min(p.l2 - j0, CPB + 1));
 
   float CB[Lay::total][W];
 #pragma unroll
@@ -80,11 +118,10 @@ __global__ __launch_bounds__(256) void sig_ho_kernel(SigArgs p) {
 #pragma unroll
     for (int w = 0; w < W; ++w) CB[k][w] = 0.0f;
 
-  const int M = p.M;
-  const int nrows = Seed::DIFF ? p.l1 - 1 : p.l1;
   RowData<DP> rd;
   rd.load(fx, 0, SEED);
   for (int i = 0; i < nrows; ++i) {
+    float *__restrict__ cr = carry + (long long)i * ncar;
     RowData<DP> rn;
     rn.load(fx, i + 1 < nrows ? i + 1 : i, SEED);
     float dM[W];
@@ -129,11 +166,11 @@ __global__ __launch_bounds__(256) void sig_ho_kernel(SigArgs p) {
               if (x < dmv) s += CB[Lay::off(m) + x][w];
             tot[w] = s;
           }
-          excl_scan_cols<W>(tot, S00);
+          excl_scan_cols<W>(tot, S00, cr + Lay::coff(m), blk, nblk);
           float Sa[ORD][W];
 #pragma unroll
           for (int x = 1; x < ORD; ++x)
-            if (x < dn) excl_scan_cols<W>(rowsum[x - 1], Sa[x]);
+            if (x < dn) excl_scan_cols<W>(rowsum[x - 1], Sa[x], cr + Lay::coff(m) + x, blk, nblk);
           // new blocks, in place: same-cell chain first (descending), then the edges
 #pragma unroll
           for (int x = ORD - 1; x >= 1; --x)
@@ -172,8 +209,6 @@ __global__ __launch_bounds__(256) void sig_ho_kernel(SigArgs p) {
     rd = rn;
   }
 
-  float K[MMAX + 1];
-  K[0] = 1.0f;
 #pragma unroll
   for (int m = 1; m <= MMAX; ++m) {
     float s = 0.0f;
@@ -181,30 +216,48 @@ __global__ __launch_bounds__(256) void sig_ho_kernel(SigArgs p) {
     for (int x = 0; x < Lay::dm(m); ++x)
 #pragma unroll
       for (int w = 0; w < W; ++w) s += CB[Lay::off(m) + x][w];
-    K[m] = group_sum<64>(s);
+    Kacc[m] += group_sum<64>(s);
   }
+  }  // column blocks
+
+  float K[MMAX + 1];
+  K[0] = 1.0f;
+#pragma unroll
+  for (int m = 1; m <= MMAX; ++m) K[m] = Kacc[m];
   if (lane == 0) {
     K[1] = level1_closed<DP, SEED>(fx, fy, p.l1, p.l2);  // ho seeds are the DIFF seeds
     store_pair<MMAX>(p, a, b, K);
   }
 }
 
+// Columns per lane for the higher-order kernel (one pair per wave): the fewest that cover the sequence,
+// up to the register budget of the order (4 for order <= 4, 2 for order 5, 1 above); longer sequences
+// run in column blocks at that width.
+static int ho_wmax(int order) { return order <= 4 ? 4 : (order <= 5 ? 2 : 1); }
+static int ho_w(int l2, int order) {
+  for (int W = 1; W < ho_wmax(order); W *= 2)
+    if (64 * W >= l2) return W;
+  return ho_wmax(order);
+}
+static int ho_blocks(int l2, int W) { return 64 * W >= l2 ? 1 : (l2 - 1 + 64 * W - 2) / (64 * W - 1); }
+// LDS of a 4-wave workgroup for the carries of a blocked launch
+static size_t ho_carry_bytes(int l1, int order, int M, int nblk) {
+  return nblk > 1 ? (size_t)4 * (l1 - 1) * ho_carries(order, M) * sizeof(float) : 0;
+}
+constexpr size_t HO_MAX_CARRY_BYTES = 160 * 1024;
+
 template <int DP, int W, int ORD, int SEED>
-static int launch_ho(const SigArgs &a, long long nblocks, hipStream_t s) {
+static int launch_ho(const SigArgs &a0, long long nblocks, hipStream_t s) {
   if (nblocks <= 0) return GPSIG_OK;
-  hipLaunchKernelGGL((sig_ho_kernel<DP, W, ORD, 8, SEED>), dim3((unsigned)nblocks), dim3(256), 0, s, a);
+  SigArgs a = a0;
+  a.nblk = ho_blocks(a.l2, W);
+  const size_t lds = ho_carry_bytes(a.l1, ORD, a.M, a.nblk);
+  if (lds > HO_MAX_CARRY_BYTES) return GPSIG_EUNSUPPORTED;
+  hipLaunchKernelGGL((sig_ho_kernel<DP, W, ORD, 8, SEED>), dim3((unsigned)nblocks), dim3(256), lds, s, a);
   return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
 }
 
-// Columns per lane for the higher-order kernel (one pair per wave); 0 = unsupported.
-static int ho_w(int l2, int order) {
-  if (l2 <= 64) return 1;
-  if (l2 <= 128 && order <= 5) return 2;
-  if (l2 <= 256 && order <= 4) return 4;
-  return 0;
-}
-
-int ho_lanes_per_pair(int l2, int order, int M) { return (M <= 8 && order <= 8 && ho_w(l2, order)) ? 64 : 0; }
+int ho_lanes_per_pair(int l2, int order, int M) { return (M <= 8 && order <= 8 && l2 >= 2) ? 64 : 0; }
 
 template <int DP, int SEED>
 static int ho_dispatch(const SigArgs &a, long long nblocks, hipStream_t s) {

@@ -47,6 +47,30 @@ def test_long_sequences_match_oracle(L, D, M, base, diff):
     assert (norm_rel_err(d[1:], np.stack([np.diagonal(e) for e in ref.K_seq(X, X)])[1:], axis_levels=True) < TOL).all()
 
 
+@pytest.mark.parametrize("L,D,M,order,base", [
+    (300, 3, 5, 2, "rbf"),       # W = 4: 255 cells per block, 2 blocks
+    (300, 4, 5, 3, "linear"),
+    (300, 3, 5, 4, "rbf"),
+    (300, 2, 5, 5, "linear"),    # W = 2: 127 cells per block, 3 blocks
+    (600, 2, 4, 2, "rbf"),       # 3 blocks
+    (200, 3, 8, 8, "linear"),    # order 8 (exact signature at M = 8): W = 1, 4 blocks of 63 cells
+])
+def test_long_higher_order_matches_oracle(L, D, M, order, base):
+    """Higher-order recursion (signature_algs.py:37-74) in column blocks: the exclusive column scans of
+    every level and block index carry across the block seams through LDS."""
+    from gpsig_amd import ops
+    X = walks(4, L, D, L + 7 * order)
+    Y = walks(2, L - 29, D, L + 7 * order + 1)
+    ref = kr.SignatureKernelRef(L * D, D, M, normalization=False, base=base, order=order)
+    got = ops.sig_gram(t(X), None, M, order=order, base=base).cpu().numpy()
+    assert (norm_rel_err(got[1:], ref.K_seq(X, X)[1:], axis_levels=True) < TOL).all()
+    got = ops.sig_gram(t(X), t(Y), M, order=order, base=base).cpu().numpy()
+    assert (norm_rel_err(got[1:], ref.K_seq(X, Y)[1:], axis_levels=True) < TOL).all()
+    d = ops.sig_diag(t(X), M, order=order, base=base).cpu().numpy()
+    exp = np.stack([np.diagonal(e) for e in ref.K_seq(X, X)])
+    assert (norm_rel_err(d[1:], exp[1:], axis_levels=True) < TOL).all()
+
+
 def test_long_normalised_K_and_saved_state_gradient_path():
     """SignatureRBF.K at L = 700 (normalised, fused epilogue) vs the oracle; the training forward (saved
     VJP state, gpsig_sig_gram_state) at the same length writes the same Gram."""
