@@ -52,6 +52,9 @@ SIGNATURES = {
     "gpsig_sig_diag": (_I, [_P, _I, _I, _I, _I, _I, _I, _I, _F, _I, _P, _P, _SZ, _P]),
     "gpsig_sig_gram_vjp": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _I,
                                 _P, _P, _P, _F, _P, _P, _P, _P, _P, _P, _P, _SZ, _P]),
+    "gpsig_sig_vjp_ho_workspace_bytes": (_SZ, [_I, _I, _I, _I, _I, _I, _I, _I]),
+    "gpsig_sig_gram_vjp_ho": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _P, _I,
+                                   _P, _P, _P, _F, _P, _P, _P, _P, _P, _P, _SZ, _P]),
     "gpsig_sig_state_bytes": (_SZ, [_I, _I, _I, _I, _I]),
     "gpsig_sig_gram_state": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _F, _I, _P,
                                   _I, _I, _P, _SZ, _P, _SZ, _P]),

@@ -14,9 +14,10 @@ When a gradient is needed, the forward Gram launch also saves its end-of-sweep s
 sweep; above GRAM_STATE_BYTES (env GPSIG_GRAM_STATE_BYTES) the VJP recomputes it instead.
 
 Gradients reach the sequences (and, through the host-side scaling in kernels.py, the lengthscales)
-and sigma * variances.  Supported for order == 1 (difference True or False), and for the Gram and its
-diagonal of SignatureLinear with order >= num_levels (the exact signature kernel; backward through the
-signature features, ops.sig_gram_ho_vjp); other higher orders evaluate forward but raise
+and sigma * variances.  Supported for order == 1 (difference True or False); for order > 1 the Gram and
+its diagonal through gpsig_sig_gram_vjp_ho (csrc/sig_ho_bwd.h: min(order, M) = 2 or 3, lengths <= 256)
+and, beyond it, for SignatureLinear with order >= num_levels (the exact signature kernel; backward
+through the signature features, ops.sig_gram_ho_vjp); other higher orders evaluate forward but raise
 NotImplementedError on backward.
 """
 from __future__ import annotations
@@ -38,13 +39,22 @@ def _ho_signature_case(cfg):
     return cfg["order"] >= cfg["num_levels"] and cfg["base"] in ("linear", "lin") and cfg["difference"]
 
 
+def _ho_vjp_kernel(cfg, *lengths):
+    """Higher order, and the higher-order VJP kernel (gpsig_sig_gram_vjp_ho) covers the sequences."""
+    return (cfg["order"] > 1 and cfg["num_levels"] > 1 and cfg["difference"]
+            and cfg["base"] in ("rbf", "linear", "lin")
+            and all(ops.ho_vjp_supported(l, cfg["num_levels"], cfg["order"], cfg["base"]) for l in lengths))
+
+
 def _check_bwd(cfg, gram=False):
     """The VJP kernels cover order 1 (difference True or False); Gram / diagonal gradients of higher
-    orders are covered for the exact signature kernel (linear, order >= num_levels)."""
+    orders are covered by the higher-order VJP kernel (checked by the caller) or, beyond it, for the
+    exact signature kernel (linear, order >= num_levels)."""
     if cfg["order"] != 1 and not (gram and _ho_signature_case(cfg)):
         raise NotImplementedError("gradients of the signature kernels are implemented for order=1 "
-                                  "(gpsig_sig_gram_vjp, gpsig_tens_vs_seq_vjp) and, for the Gram and its "
-                                  "diagonal, for SignatureLinear with order >= num_levels")
+                                  "(gpsig_sig_gram_vjp, gpsig_tens_vs_seq_vjp), for the Gram and its diagonal "
+                                  "at min(order, num_levels) in (2, 3) up to length 256 (gpsig_sig_gram_vjp_ho), "
+                                  "and for SignatureLinear with order >= num_levels")
 
 
 def _ho_gram_backward(ctx, gout):
@@ -116,10 +126,12 @@ class SigGram(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gout):
         cfg = ctx.cfg
-        _check_bwd(cfg, gram=True)
-        if cfg["order"] != 1:
-            return _ho_gram_backward(ctx, gout)
         Xs, X2s, sc32, rs1, rs2 = ctx.saved_tensors
+        lengths = (Xs.shape[1],) if X2s is None else (Xs.shape[1], X2s.shape[1])
+        if cfg["order"] != 1 and not _ho_vjp_kernel(cfg, *lengths):
+            _check_bwd(cfg, gram=True)
+            return _ho_gram_backward(ctx, gout)
+        order = cfg["order"]
         M = cfg["num_levels"]
         sym = X2s is None
         dev = Xs.device
@@ -132,18 +144,17 @@ class SigGram(torch.autograd.Function):
         gscale = torch.zeros((M + 1,), dtype=torch.float32, device=dev)
         jit = cfg["jitter"] if (cfg["normalization"] and sym) else 0.0
         gX, gY = ops.sig_gram_vjp(Xs.detach(), None if sym else X2s.detach(), M, gout, base=cfg["base"],
-                                  difference=cfg["difference"],
+                                  difference=cfg["difference"], order=order,
                                   gout_levels=cfg["return_levels"], rs1=rs1, rs2=rs2, scale=sc32, jitter=jit,
                                   grs1=grs1, grs2=grs2, gscale=gscale, state=ctx.state)
         ctx.state = None
         if cfg["normalization"]:
             # rs = (K_m(a, a) + jitter)^-1/2  ->  dLoss/dK_m(a, a) = -rs^3/2 dLoss/drs
             ops.sig_gram_vjp(Xs.detach(), None, M, grs1 * (-0.5) * rs1 ** 3, base=cfg["base"], diag=True, gX=gX,
-                             difference=cfg["difference"])
+                             difference=cfg["difference"], order=order)
             if not sym:
                 ops.sig_gram_vjp(X2s.detach(), None, M, grs2 * (-0.5) * rs2 ** 3, base=cfg["base"], diag=True,
-                                 difference=cfg["difference"],
-                                 gX=gY)
+                                 difference=cfg["difference"], order=order, gX=gY)
         gXo = gX.to(Xs.dtype) if ctx.needs_input_grad[0] else None
         gYo = gY.to(X2s.dtype) if (not sym and ctx.needs_input_grad[1]) else None
         gso = gscale.to(ctx.scale_dtype) if ctx.needs_input_grad[2] else None
@@ -162,13 +173,13 @@ class SigDiag(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gout):
         cfg = ctx.cfg
-        _check_bwd(cfg, gram=True)
         (Xs,) = ctx.saved_tensors
-        if cfg["order"] != 1:
+        if cfg["order"] != 1 and not _ho_vjp_kernel(cfg, Xs.shape[1]):
+            _check_bwd(cfg, gram=True)
             gX, _ = ops.sig_gram_ho_vjp(Xs.detach(), None, cfg["num_levels"], None, gout)
         else:
             gX, _ = ops.sig_gram_vjp(Xs.detach(), None, cfg["num_levels"], gout, base=cfg["base"], diag=True,
-                                     difference=cfg["difference"])
+                                     difference=cfg["difference"], order=cfg["order"])
         return gX.to(Xs.dtype), None
 
 

@@ -8,7 +8,8 @@ int features(const float *X, int n, int l, int d, int DP, float *F, hipStream_t 
 int fo_fixed_max();
 size_t sig_bwd_wide_workspace(int n1, int l1, int n2, int l2, int d);
 int sig_bwd_wide(BwdArgs a, const float *X, const float *Y, int seed, void *workspace, size_t workspace_bytes,
-                 hipStream_t s);
+                 hipStream_t s, int order = 1);
+bool ho_bwd_supported(int l2, int order, int M, int seed);
 // channel counts past the VJP's instantiations (or past the forward's crossover): the wide-channel VJP
 static bool bwd_wide(int d) { return d > 16 || d > fo_fixed_max(); }
 template <int DP, int M>
@@ -50,6 +51,48 @@ __global__ void gscale_reduce_kernel(const float *__restrict__ slots, int levels
 }
 static inline long long upper_prefix(long long r, long long ntb, long long k) { return r * ntb - k * r * (r - 1) / 2; }
 
+// The VJPs with point-weight tiles and emission GEMMs (sig_bwd_wide.hip): order 1 at wide channel counts,
+// and every order > 1
+static int tile_vjp(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int num_levels, int order,
+                    int seed, int pair_mode, int row_begin, int row_end, const float *gout, int gout_levels,
+                    const float *rs1, const float *rs2, const float *scale, float jitter, float *gX, float *gY,
+                    float *grs1, float *grs2, float *gscale, const float *state, void *workspace,
+                    size_t workspace_bytes, hipStream_t s) {
+  if (row_end == row_begin) return GPSIG_OK;
+  if (!workspace || workspace_bytes < GSC_BYTES + sig_bwd_wide_workspace(n1, l1, n2, l2, d)) return GPSIG_EWORKSPACE;
+  float *gsc_slots = static_cast<float *>(workspace);
+  BwdArgs a{};
+  a.n1 = n1; a.l1 = l1; a.n2 = n2; a.l2 = l2; a.d = d;
+  a.M = num_levels;
+  a.pair_mode = pair_mode;
+  a.row_begin = row_begin;
+  a.row_end = row_end;
+  a.gout = gout;
+  a.gout_levels = gout_levels ? 1 : 0;
+  a.g_ld = n2;
+  a.g_lvl = pair_mode == GPSIG_PAIRS_DIAG ? (long long)n1 : (long long)n1 * n2;
+  a.rs1 = rs1; a.rs2 = rs2; a.scale = scale;
+  a.jitter = jitter;
+  a.gX = gX;
+  a.gY = pair_mode == GPSIG_PAIRS_RECT ? gY : gX;
+  a.grs1 = grs1;
+  a.grs2 = pair_mode == GPSIG_PAIRS_RECT ? grs2 : grs1;
+  a.gscale = nullptr;
+  if (gscale && pair_mode != GPSIG_PAIRS_DIAG) {
+    if (hipMemsetAsync(gsc_slots, 0, GSC_BYTES, s) != hipSuccess) return GPSIG_ELAUNCH;
+    a.gscale = gsc_slots;
+  }
+  a.state = state;
+  const int rc = sig_bwd_wide(a, X, pair_mode == GPSIG_PAIRS_RECT ? Y : X, seed, static_cast<char *>(workspace) + GSC_BYTES,
+                              workspace_bytes - GSC_BYTES, s, order);
+  if (rc) return rc;
+  if (a.gscale) {
+    hipLaunchKernelGGL(gscale_reduce_kernel, dim3(1), dim3(64), 0, s, gsc_slots, num_levels + 1, gscale);
+    if (hipGetLastError() != hipSuccess) return GPSIG_ELAUNCH;
+  }
+  return GPSIG_OK;
+}
+
 }  // namespace gpsig
 
 using namespace gpsig;
@@ -75,41 +118,9 @@ extern "C" int gpsig_sig_gram_vjp(const float *X, int n1, int l1, const float *Y
   const bool wide = bwd_wide(d);
   const int DP = wide ? 0 : bwd_pad(d);
   if (seed < 0 || (DP == 0 && !wide) || num_levels > 8) return GPSIG_EUNSUPPORTED;
-  if (wide) {
-    if (row_end == row_begin) return GPSIG_OK;
-    if (!workspace || workspace_bytes < GSC_BYTES + sig_bwd_wide_workspace(n1, l1, n2, l2, d)) return GPSIG_EWORKSPACE;
-    float *gsc_slots = static_cast<float *>(workspace);
-    BwdArgs a{};
-    a.n1 = n1; a.l1 = l1; a.n2 = n2; a.l2 = l2; a.d = d;
-    a.M = num_levels;
-    a.pair_mode = pair_mode;
-    a.row_begin = row_begin;
-    a.row_end = row_end;
-    a.gout = gout;
-    a.gout_levels = gout_levels ? 1 : 0;
-    a.g_ld = n2;
-    a.g_lvl = pair_mode == GPSIG_PAIRS_DIAG ? (long long)n1 : (long long)n1 * n2;
-    a.rs1 = rs1; a.rs2 = rs2; a.scale = scale;
-    a.jitter = jitter;
-    a.gX = gX;
-    a.gY = pair_mode == GPSIG_PAIRS_RECT ? gY : gX;
-    a.grs1 = grs1;
-    a.grs2 = pair_mode == GPSIG_PAIRS_RECT ? grs2 : grs1;
-    a.gscale = nullptr;
-    if (gscale && pair_mode != GPSIG_PAIRS_DIAG) {
-      if (hipMemsetAsync(gsc_slots, 0, GSC_BYTES, s) != hipSuccess) return GPSIG_ELAUNCH;
-      a.gscale = gsc_slots;
-    }
-    a.state = state;
-    const int rc = sig_bwd_wide(a, X, pair_mode == GPSIG_PAIRS_RECT ? Y : X, seed, static_cast<char *>(workspace) + GSC_BYTES,
-                                workspace_bytes - GSC_BYTES, s);
-    if (rc) return rc;
-    if (a.gscale) {
-      hipLaunchKernelGGL(gscale_reduce_kernel, dim3(1), dim3(64), 0, s, gsc_slots, num_levels + 1, gscale);
-      if (hipGetLastError() != hipSuccess) return GPSIG_ELAUNCH;
-    }
-    return GPSIG_OK;
-  }
+  if (wide)
+    return tile_vjp(X, n1, l1, Y, n2, l2, d, num_levels, 1, seed, pair_mode, row_begin, row_end, gout, gout_levels,
+                    rs1, rs2, scale, jitter, gX, gY, grs1, grs2, gscale, state, workspace, workspace_bytes, s);
   const BwdGeo geo = bwd_geometry(l2, DP);
   if (geo.W == 0) return GPSIG_EUNSUPPORTED;
   if (row_end == row_begin) return GPSIG_OK;
@@ -207,4 +218,38 @@ extern "C" size_t gpsig_sig_vjp_workspace_bytes(int n1, int l1, int n2, int l2, 
   return align256((size_t)n1 * l1 * feat_stride(DP) * sizeof(float)) +
          align256((size_t)n2 * l2 * feat_stride(DP) * sizeof(float)) + (size_t)scr * 4 * BWD_CHUNK_BLOCKS * sizeof(float) +
          GSC_BYTES;
+}
+
+extern "C" int gpsig_sig_gram_vjp_ho(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d,
+                                     int num_levels, int order, int base_kind, int pair_mode, int row_begin,
+                                     int row_end, const float *gout, int gout_levels, const float *rs1,
+                                     const float *rs2, const float *scale, float jitter, float *gX, float *gY,
+                                     float *grs1, float *grs2, float *gscale, void *workspace,
+                                     size_t workspace_bytes, gpsig_stream_t stream) {
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (!X || !Y || !gout || !gX || n1 <= 0 || n2 <= 0 || d <= 0 || num_levels < 1 || order < 1) return GPSIG_EINVAL;
+  if (l1 < 2 || l2 < 2) return GPSIG_EINVAL;
+  if (pair_mode < GPSIG_PAIRS_RECT || pair_mode > GPSIG_PAIRS_DIAG) return GPSIG_EINVAL;
+  if (row_begin < 0 || row_end > n1 || row_begin > row_end) return GPSIG_EINVAL;
+  if (pair_mode != GPSIG_PAIRS_RECT && (n1 != n2 || l1 != l2 || X != Y)) return GPSIG_EINVAL;
+  if (pair_mode == GPSIG_PAIRS_RECT && !gY) return GPSIG_EINVAL;
+  if (pair_mode == GPSIG_PAIRS_DIAG && !gout_levels) return GPSIG_EINVAL;
+  if ((rs1 == nullptr) != (rs2 == nullptr)) return GPSIG_EINVAL;
+  if (order == 1 || num_levels == 1)  // the first-order recursion
+    return gpsig_sig_gram_vjp(X, n1, l1, Y, n2, l2, d, num_levels, base_kind, 1, pair_mode, row_begin, row_end, gout,
+                              gout_levels, rs1, rs2, scale, jitter, gX, gY, grs1, grs2, gscale, nullptr, workspace,
+                              workspace_bytes, stream);
+  const int seed = base_kind == GPSIG_BASE_RBF ? SEED_RBF_DIFF : base_kind == GPSIG_BASE_LINEAR ? SEED_LIN_DIFF : -1;
+  if (seed < 0 || !ho_bwd_supported(l2, order, num_levels, seed)) return GPSIG_EUNSUPPORTED;
+  return tile_vjp(X, n1, l1, Y, n2, l2, d, num_levels, order, seed, pair_mode, row_begin, row_end, gout, gout_levels,
+                  rs1, rs2, scale, jitter, gX, gY, grs1, grs2, gscale, nullptr, workspace, workspace_bytes, s);
+}
+
+extern "C" size_t gpsig_sig_vjp_ho_workspace_bytes(int n1, int l1, int n2, int l2, int d, int num_levels, int order,
+                                                   int base_kind) {
+  if (n1 <= 0 || n2 <= 0 || l1 < 2 || l2 < 2 || d <= 0 || order < 1) return 0;
+  if (order == 1 || num_levels == 1) return gpsig_sig_vjp_workspace_bytes(n1, l1, n2, l2, d, num_levels, 1);
+  const int seed = base_kind == GPSIG_BASE_RBF ? SEED_RBF_DIFF : base_kind == GPSIG_BASE_LINEAR ? SEED_LIN_DIFF : -1;
+  if (seed < 0 || !ho_bwd_supported(l2, order, num_levels, seed)) return 0;
+  return GSC_BYTES + sig_bwd_wide_workspace(n1, l1, n2, l2, d);
 }

@@ -15,7 +15,7 @@
 // WideSeedGen: the chunk's dots, the exp-free recurrences, exact rows), WIDE_R rows at a time, into the
 // lane's LDS slots.
 #pragma once
-#include "sig_bwd.h"
+#include "bwd_pair.h"
 #include "wide.h"
 
 namespace gpsig {
@@ -179,69 +179,10 @@ __global__ __launch_bounds__(256) void sig_bwd_wide_kernel(BwdArgs p) {
     if constexpr (DIFF) K[1] = level1_closed_wide<SEED>(fx, fy, p.wd, p.lw1, p.lw2, l1, l2);
   }
 
-  // ---- per-level weights g_m = dLoss/dK_m(a, b) and the normalisation / scale terms (as sig_bwd.h)
-  const bool upper_off = p.pair_mode == GPSIG_PAIRS_UPPER && a != bl;
-  const float jit = (p.pair_mode == GPSIG_PAIRS_UPPER && a == bl) ? p.jitter : 0.0f;
-  auto pair_terms = [&](float (&gs)[M + 1], float (&sc)[M + 1], float (&r1)[M + 1], float (&r2)[M + 1]) {
-    float gsum = 0.0f;
-    if (!diag && !p.gout_levels) {
-      gsum = p.gout[(long long)a * p.g_ld + bl];
-      if (upper_off) gsum += p.gout[(long long)bl * p.g_ld + a];
-    }
-#pragma unroll
-    for (int m = 0; m <= M; ++m) {
-      float gv;
-      if (diag) {
-        gv = p.gout[(long long)m * p.g_lvl + a];
-      } else if (p.gout_levels) {
-        gv = p.gout[(long long)m * p.g_lvl + (long long)a * p.g_ld + bl];
-        if (upper_off) gv += p.gout[(long long)m * p.g_lvl + (long long)bl * p.g_ld + a];
-      } else {
-        gv = gsum;
-      }
-      gs[m] = pair_ok ? gv : 0.0f;
-      sc[m] = p.scale ? p.scale[m] : 1.0f;
-      r1[m] = p.rs1 ? p.rs1[(long long)m * p.n1 + a] : 1.0f;
-      r2[m] = p.rs2 ? p.rs2[(long long)m * p.n2 + bl] : 1.0f;
-    }
-  };
+  // ---- per-level weights g_m = dLoss/dK_m(a, b) and the normalisation / scale terms (bwd_pair.h)
+  const PairTerms<M> pt(p, a, bl, gl, pair_ok, lblk);
   float gw[M + 1];
-  {
-    float gs[M + 1], sc[M + 1], r1[M + 1], r2[M + 1];
-    pair_terms(gs, sc, r1, r2);
-#pragma unroll
-    for (int m = 0; m <= M; ++m) gw[m] = gs[m] * sc[m] * r1[m] * r2[m];
-  }
-  auto norm_terms = [&]() {
-    if (diag || !(p.gscale || (p.rs1 && (p.grs1 || p.grs2)))) return;
-    float gs[M + 1], sc[M + 1], r1[M + 1], r2[M + 1];
-    pair_terms(gs, sc, r1, r2);
-    const bool lead = gl == 0 && pair_ok;
-    float g1[M + 1], g2[M + 1], gsc[M + 1];
-#pragma unroll
-    for (int m = 0; m <= M; ++m) {
-      const float t = gs[m] * sc[m] * (K[m] + jit);
-      g1[m] = lead ? t * r2[m] : 0.0f;
-      g2[m] = t * r1[m];
-      gsc[m] = lead ? gs[m] * (K[m] + jit) * r1[m] * r2[m] : 0.0f;
-    }
-    if (p.rs1 && p.grs1) {
-      wave_sum_last_n<M + 1>(g1);
-      if (lane == 63)
-        for (int m = 0; m <= M; ++m) unsafeAtomicAdd(p.grs1 + (long long)m * p.n1 + a, g1[m]);
-    }
-    if (p.rs1 && p.grs2 && lead) {
-#pragma unroll
-      for (int m = 0; m <= M; ++m) unsafeAtomicAdd(p.grs2 + (long long)m * p.n2 + bl, g2[m]);
-    }
-    if (p.gscale) {
-      wave_sum_last_n<M + 1>(gsc);
-      if (lane == 63) {
-        float *slot = p.gscale + (long long)(lblk & (GSCALE_SLOTS - 1)) * (M + 1);
-        for (int m = 0; m <= M; ++m) unsafeAtomicAdd(slot + m, gsc[m]);
-      }
-    }
-  };
+  pt.weights(gw);
 
   // ---- point weights of this pair into the tile: row pi of the pair's l1 x l2 block
   float *__restrict__ tpair = p.tile + (long long)(a - p.tile_a0) * p.tile_as +
@@ -354,7 +295,7 @@ __global__ __launch_bounds__(256) void sig_bwd_wide_kernel(BwdArgs p) {
     for (int w = 0; w < W; ++w) Kh[w] = -Ep[w];
     emit(0, Kh, kr1);
   }
-  norm_terms();
+  pt.norm(K);
 }
 
 // Geometry of the wide VJP: the forward's (W = 8, LP = 16/32/64), one column block (l2 <= 512).

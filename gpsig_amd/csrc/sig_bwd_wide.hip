@@ -12,6 +12,8 @@ int gemm_f32(hipStream_t s, bool transA, bool transB, int M, int N, int K, float
 size_t gemm_splitk_bytes(int M, int N, int K);
 template <int M>
 int sig_bwd_wide_launch_m(const BwdArgs &a, int seed, long long nblocks, hipStream_t s);
+bool ho_bwd_supported(int l2, int order, int M, int seed);
+int sig_ho_bwd_launch(const BwdArgs &a, int order, int seed, long long nblocks, hipStream_t s);
 
 // Xa[r][k] = X[r][k] (k < d), Xa[r][d] = 1
 __global__ __launch_bounds__(256) void aug_ones_kernel(const float *__restrict__ X, long long rows, int d,
@@ -82,13 +84,14 @@ size_t sig_bwd_wide_workspace(int n1, int l1, int n2, int l2, int d) {
   return best;
 }
 
-// The wide-channel VJP.  a: filled by the caller as for the fixed kernels (pair mode, rows, gout, rs, scale,
-// jitter, gX/gY/grs, gscale slots, state); X, Y the raw (n, l, d) inputs.
+// The wide-channel VJP (order 1) and the higher-order VJP (order > 1, sig_ho_bwd.h: one pair per wave, the
+// same tiles and GEMMs).  a: filled by the caller as for the fixed kernels (pair mode, rows, gout, rs,
+// scale, jitter, gX/gY/grs, gscale slots, state); X, Y the raw (n, l, d) inputs.
 int sig_bwd_wide(BwdArgs a, const float *X, const float *Y, int seed, void *workspace, size_t workspace_bytes,
-                 hipStream_t s) {
+                 hipStream_t s, int order) {
   const int n1 = a.n1, l1 = a.l1, n2 = a.n2, l2 = a.l2, d = a.d, pm = a.pair_mode;
-  if (l2 > 512) return GPSIG_EUNSUPPORTED;  // one column block
-  const BwdGeo geo = bwd_geometry_wide(l2);
+  if (order > 1 ? !ho_bwd_supported(l2, order, a.M, seed) || a.state : l2 > 512) return GPSIG_EUNSUPPORTED;
+  const BwdGeo geo = order > 1 ? BwdGeo{4, 64} : bwd_geometry_wide(l2);
   const WidePlan pl = wide_plan(n1, l1, n2, l2, d, pm);
   if (!workspace || workspace_bytes < plan_bytes(pl)) return GPSIG_EWORKSPACE;
   char *w = static_cast<char *>(workspace);
@@ -166,7 +169,9 @@ int sig_bwd_wide(BwdArgs a, const float *X, const float *Y, int seed, void *work
         return GPSIG_ELAUNCH;
     }
     if (nblocks > 0x7fffffffLL) return GPSIG_EUNSUPPORTED;
-    if (nblocks > 0) {
+    if (nblocks > 0 && order > 1) {
+      if ((rc = sig_ho_bwd_launch(c, order, seed, nblocks, s))) return rc;
+    } else if (nblocks > 0) {
       switch (a.M) {
         case 1: rc = sig_bwd_wide_launch_m<1>(c, seed, nblocks, s); break;
         case 2: rc = sig_bwd_wide_launch_m<2>(c, seed, nblocks, s); break;

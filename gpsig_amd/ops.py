@@ -228,11 +228,12 @@ def sig_gram_vjp(X: torch.Tensor, Y: torch.Tensor | None, num_levels: int, gout:
                  gout_levels: bool = False, diag: bool = False, rs1=None, rs2=None, scale=None, jitter: float = 0.0,
                  gX: torch.Tensor | None = None, gY: torch.Tensor | None = None, grs1=None, grs2=None,
                  gscale=None, rows: tuple | None = None, state: torch.Tensor | None = None,
-                 difference: bool = True):
-    """dLoss/dX (and dLoss/dY, dLoss/drs, dLoss/dscale) of the first-order Gram, accumulated into float32
-    buffers: see gpsig_sig_gram_vjp in include/gpsig_amd.h.  Y None -> symmetric K(X) (or the diagonal
-    with diag=True; gout is then (num_levels+1, n) per level).  state: the buffer a sig_gram(...,
-    state=) call on the same inputs filled -> the forward sweep is skipped.  Returns (gX, gY)."""
+                 difference: bool = True, order: int = 1):
+    """dLoss/dX (and dLoss/dY, dLoss/drs, dLoss/dscale) of the Gram, accumulated into float32 buffers: see
+    gpsig_sig_gram_vjp (order 1) and gpsig_sig_gram_vjp_ho (order > 1) in include/gpsig_amd.h.  Y None ->
+    symmetric K(X) (or the diagonal with diag=True; gout is then (num_levels+1, n) per level).  state: the
+    buffer a sig_gram(..., state=) call on the same inputs filled -> the forward sweep is skipped (order 1).
+    Returns (gX, gY)."""
     _require_cuda(X, Y, gout, rs1, rs2, scale)
     lib = L.load()
     X = _f32(X)
@@ -267,9 +268,24 @@ def sig_gram_vjp(X: torch.Tensor, Y: torch.Tensor | None, num_levels: int, gout:
         rs1, rs2 = _f32(rs1), _f32(rs2)
     if scale is not None:
         scale = _f32(scale)
+    mode = L.PAIRS_DIAG if diag else (L.PAIRS_UPPER if sym else L.PAIRS_RECT)
+    if order > 1 and num_levels > 1:
+        if state is not None or not difference:
+            raise ValueError("the higher-order VJP takes difference=True and no saved state")
+        nb = lib.gpsig_sig_vjp_ho_workspace_bytes(n1, l1, n2, l2, d, num_levels, order, base_kind(base))
+        if nb == 0:
+            L.check(L.GPSIG_EUNSUPPORTED, f"gpsig_sig_gram_vjp_ho (order {order}, num_levels {num_levels}, "
+                                          f"length {l2})")
+        ws = workspace(X.device, nb)
+        rc = lib.gpsig_sig_gram_vjp_ho(X.data_ptr(), n1, l1, Y.data_ptr(), n2, l2, d, num_levels, order,
+                                       base_kind(base), mode, r0, r1, gout.data_ptr(), int(bool(gout_levels)),
+                                       _ptr(rs1), _ptr(rs2), _ptr(scale), float(jitter), gX.data_ptr(), _ptr(gY),
+                                       _ptr(grs1), _ptr(grs2), _ptr(gscale), ws.data_ptr(), ws.numel(),
+                                       _stream(X.device))
+        L.check(rc, "gpsig_sig_gram_vjp_ho")
+        return gX, gY
     nb = lib.gpsig_sig_vjp_workspace_bytes(n1, l1, n2, l2, d, num_levels, int(bool(difference)))
     ws = workspace(X.device, nb)
-    mode = L.PAIRS_DIAG if diag else (L.PAIRS_UPPER if sym else L.PAIRS_RECT)
     rc = lib.gpsig_sig_gram_vjp(X.data_ptr(), n1, l1, Y.data_ptr(), n2, l2, d, num_levels, base_kind(base),
                                 int(bool(difference)), mode, r0, r1,
                                 gout.data_ptr(), int(bool(gout_levels)), _ptr(rs1), _ptr(rs2), _ptr(scale),
@@ -425,6 +441,11 @@ def pde_vjp_fronts(X: torch.Tensor, Y: torch.Tensor | None, gout: torch.Tensor, 
 
 
 # ----------------------------------------------------------------------------- signature features
+def ho_vjp_supported(l2: int, num_levels: int, order: int, base="rbf") -> bool:
+    """Whether gpsig_sig_gram_vjp_ho covers (length, levels, order, base kernel)."""
+    return L.load().gpsig_sig_vjp_ho_workspace_bytes(1, 2, 1, l2, 1, num_levels, order, base_kind(base)) > 0
+
+
 def sig_gram_ho_vjp(X: torch.Tensor, Y: torch.Tensor | None, num_levels: int, gK: torch.Tensor | None,
                     gd1: torch.Tensor | None = None, gd2: torch.Tensor | None = None):
     """dLoss/dX, dLoss/dY of the raw per-level higher-order Gram of the linear base kernel with

@@ -136,7 +136,9 @@ int gpsig_sig_diag(const float *X, int n, int l, int d, int num_levels, int orde
  *   Workspace: gpsig_sig_vjp_workspace_bytes(n1, l1, n2, l2, d, num_levels, difference): the feature
  *   records, for sequences longer than one lane group covers (column blocks) the per-row carries of
  *   one launch chunk, and the partial sums of gscale (reduced into gscale after the launch, on the
- *   same stream).  Any length; d <= 16.
+ *   same stream).  Any length up to 16 channels; above 16 (wide channels) l2 <= 512, the point weights
+ *   of a chunk of pairs go to a tile in the workspace and the matrix-core GEMMs (gpsig_gemm_f32) contract
+ *   them with the points.
  */
 size_t gpsig_sig_vjp_workspace_bytes(int n1, int l1, int n2, int l2, int d, int num_levels, int difference);
 int gpsig_sig_gram_vjp(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int num_levels,
@@ -144,6 +146,19 @@ int gpsig_sig_gram_vjp(const float *X, int n1, int l1, const float *Y, int n2, i
                        const float *rs1, const float *rs2, const float *scale, float jitter, float *gX, float *gY,
                        float *grs1, float *grs2, float *gscale, const float *state, void *workspace,
                        size_t workspace_bytes, gpsig_stream_t stream);
+
+/* Gradient of the higher-order Gram (order > 1): TF autodiff of signature_kern_higher_order
+ * (signature_algs.py:37-74) behind _K_seq / K.  Arguments as gpsig_sig_gram_vjp (difference = 1, no
+ * saved state); order 1 forwards to it.  Supported: RBF / linear, any channel count, l2 <= 256, and
+ * min(order, num_levels) == 2 (num_levels <= 8) or 3 (num_levels <= 5); otherwise
+ * GPSIG_EUNSUPPORTED, and the workspace query returns 0. */
+size_t gpsig_sig_vjp_ho_workspace_bytes(int n1, int l1, int n2, int l2, int d, int num_levels, int order,
+                                        int base_kind);
+int gpsig_sig_gram_vjp_ho(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int num_levels,
+                          int order, int base_kind, int pair_mode, int row_begin, int row_end, const float *gout,
+                          int gout_levels, const float *rs1, const float *rs2, const float *scale, float jitter,
+                          float *gX, float *gY, float *grs1, float *grs2, float *gscale, void *workspace,
+                          size_t workspace_bytes, gpsig_stream_t stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Inducing tensors (sparse rank-1 tensors z = (z_{m,1} (x) ... (x) z_{m,m})_m).

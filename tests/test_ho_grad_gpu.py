@@ -82,3 +82,82 @@ def test_unsupported_higher_order_gradients_raise():
         K = k.K(X)
         with pytest.raises(NotImplementedError):
             K.sum().backward()
+
+
+def _walks(n, l, d, seed):
+    return np.cumsum(np.random.default_rng(seed).standard_normal((n, l, d)), 1) / np.sqrt(l * d)
+
+
+@pytest.mark.parametrize("L,D,M,order,base", [
+    (12, 3, 3, 2, "rbf"), (30, 4, 5, 2, "linear"), (40, 46, 4, 2, "rbf"), (200, 3, 4, 2, "rbf"),
+    (25, 3, 4, 3, "rbf"), (20, 2, 5, 3, "linear"), (18, 3, 3, 3, "linear"), (16, 2, 8, 2, "rbf"),
+])
+def test_higher_order_vjp_kernel_raw_levels(L, D, M, order, base):
+    """gpsig_sig_gram_vjp_ho (csrc/sig_ho_bwd.h) against fp64 autodiff of signature_kern_higher_order
+    (signature_algs.py:37-74, restated in oracle/autodiff_ref.py): per-level upstream gradients, cross
+    K(X, Y), symmetric K(X) (UPPER pairs) and the diagonal."""
+    from gpsig_amd import ops
+    X, Y = _walks(3, L, D, L + order), _walks(4, L - 3, D, L + order + 1)
+    G = np.random.default_rng(7).standard_normal((M + 1, 3, 4))
+    Gs = np.random.default_rng(8).standard_normal((M + 1, 3, 3))
+    Gd = np.random.default_rng(9).standard_normal((M + 1, 3))
+    Xt, Yt = torch.tensor(X, device=DEV, dtype=torch.float32), torch.tensor(Y, device=DEV, dtype=torch.float32)
+    gX, gY = ops.sig_gram_vjp(Xt, Yt, M, torch.tensor(G, device=DEV), base=base, gout_levels=True, order=order)
+    Xr, Yr = torch.tensor(X, requires_grad=True), torch.tensor(Y, requires_grad=True)
+    (ar.k_seq(Xr, Yr, M, base, order=order) * torch.tensor(G)).sum().backward()
+    assert norm_rel_err(gX.cpu().numpy(), Xr.grad.numpy()) < GTOL
+    assert norm_rel_err(gY.cpu().numpy(), Yr.grad.numpy()) < GTOL
+    gS, _ = ops.sig_gram_vjp(Xt, None, M, torch.tensor(Gs, device=DEV), base=base, gout_levels=True, order=order)
+    Xr = torch.tensor(X, requires_grad=True)
+    (ar.k_seq(Xr, Xr, M, base, order=order) * torch.tensor(Gs)).sum().backward()
+    assert norm_rel_err(gS.cpu().numpy(), Xr.grad.numpy()) < GTOL
+    gD, _ = ops.sig_gram_vjp(Xt, None, M, torch.tensor(Gd, device=DEV), base=base, diag=True, order=order)
+    Xr = torch.tensor(X, requires_grad=True)
+    (ar.k_seq_diag(Xr, M, base, order=order) * torch.tensor(Gd)).sum().backward()
+    assert norm_rel_err(gD.cpu().numpy(), Xr.grad.numpy()) < GTOL
+
+
+@pytest.mark.parametrize("cross", [False, True])
+@pytest.mark.parametrize("base", ["rbf", "linear"])
+def test_higher_order_normalised_K_gradient(cross, base):
+    """SignatureKernel(order=2).K normalised, through autograd: sequences, lengthscales and variances, vs
+    fp64 autodiff of the reference graph (kernels.py:402-477 over signature_algs.py:37-74)."""
+    import gpsig_amd
+    N, L, D, M = 5, 24, 3, 4
+    X = _walks(N, L, D, 11)
+    X2 = _walks(3, L + 4, D, 12) if cross else None
+    G = np.random.default_rng(13).standard_normal((N, 3 if cross else N))
+    ls = np.array([0.8, 1.2, 1.0])
+    var = np.linspace(0.5, 1.5, M + 1)
+    cls = gpsig_amd.SignatureRBF if base == "rbf" else gpsig_amd.SignatureLinear
+    k = cls(L * D, D, M, order=2)
+    k.lengthscales = torch.tensor(ls, device=DEV, requires_grad=True)
+    k.variances = torch.tensor(var, device=DEV, requires_grad=True)
+    Xt = torch.tensor(X.reshape(N, -1), device=DEV, requires_grad=True)
+    X2t = None if X2 is None else torch.tensor(X2.reshape(3, -1), device=DEV, requires_grad=True)
+    K = k.K(Xt, X2t)
+    (K * torch.as_tensor(G, device=DEV)).sum().backward()
+    Xr = torch.tensor(X, requires_grad=True)
+    X2r = None if X2 is None else torch.tensor(X2, requires_grad=True)
+    lr, vr = torch.tensor(ls, requires_grad=True), torch.tensor(var, requires_grad=True)
+    Kr = ar.K(Xr / lr, None if X2r is None else X2r / lr, M, base=base, scale=vr, order=2)
+    (Kr * torch.tensor(G)).sum().backward()
+    assert norm_rel_err(K.detach().cpu().numpy(), Kr.detach().numpy()) < 1e-5
+    assert norm_rel_err(Xt.grad.reshape(X.shape).cpu().numpy(), Xr.grad.numpy()) < GTOL
+    if cross:
+        assert norm_rel_err(X2t.grad.reshape(X2.shape).cpu().numpy(), X2r.grad.numpy()) < GTOL
+    assert norm_rel_err(k.lengthscales.grad.cpu().numpy(), lr.grad.numpy()) < GTOL
+    assert norm_rel_err(k.variances.grad.cpu().numpy(), vr.grad.numpy()) < GTOL
+
+
+def test_higher_order_vjp_unsupported_raises():
+    """min(order, M) = 4 and sequences past 256 points are outside the VJP kernel: the error names the
+    entry point (autograd then uses the signature-feature path for the exact linear kernel, or raises)."""
+    from gpsig_amd import _lib as Lb
+    from gpsig_amd import ops
+    X = torch.zeros((2, 10, 2), device=DEV)
+    with pytest.raises(Lb.GpsigError):
+        ops.sig_gram_vjp(X, None, 5, torch.zeros((6, 2, 2), device=DEV), gout_levels=True, order=4)
+    X = torch.zeros((2, 300, 2), device=DEV)
+    with pytest.raises(Lb.GpsigError):
+        ops.sig_gram_vjp(X, None, 3, torch.zeros((4, 2, 2), device=DEV), gout_levels=True, order=2)
