@@ -370,10 +370,12 @@ __global__ __launch_bounds__(256) void pde_rep_kernel(PdeArgs p) {
 // LDS of a pde_rep_kernel launch: the 4 waves' coarse x increments, then (column blocks only) their
 // boundary-column slabs
 template <typename T, int DP, int W, int REP>
-static size_t pde_rep_lds(int l1, int l2) {
-  const size_t dx = ((size_t)4 * (l1 - 1) * DP + 3) & ~(size_t)3;
-  const int J = REP * (l2 - 1);
-  const size_t bnd = J > 64 * W ? (size_t)4 * (REP * (l1 - 1) + 1) * sizeof(T) : 0;
+static size_t pde_rep_lds(int l1, int l2, int sub) {
+  // sub > 0 (tile mode): the kernel's coarse cells are the tile's split 2^sub ways
+  const long long IC = (long long)(l1 - 1) << sub, JC = (long long)(l2 - 1) << sub;
+  const size_t dx = ((size_t)4 * IC * DP + 3) & ~(size_t)3;
+  const long long J = REP * JC;
+  const size_t bnd = J > 64 * W ? (size_t)4 * (REP * IC + 1) * sizeof(T) : 0;
   return dx * sizeof(float) + bnd;
 }
 
@@ -382,7 +384,7 @@ static int launch_pde_rep(const PdeArgs &a, long long nblocks, hipStream_t s) {
   if constexpr ((W / REP) * DP > 64) {
     return -1;  // the per-row kernel keeps fewer increments in registers
   } else {
-    const size_t lds = pde_rep_lds<T, DP, W, REP>(a.l1, a.l2);
+    const size_t lds = pde_rep_lds<T, DP, W, REP>(a.l1, a.l2, a.inc ? a.sub : 0);
     if (lds > 160 * 1024) return GPSIG_EUNSUPPORTED;
     if (a.solver == 1)
       hipLaunchKernelGGL((pde_rep_kernel<T, DP, W, REP, 1>), dim3((unsigned)nblocks), dim3(256), lds, s, a);

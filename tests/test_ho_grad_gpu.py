@@ -75,10 +75,11 @@ def test_higher_order_diag_and_norms_gradient():
 
 
 def test_unsupported_higher_order_gradients_raise():
-    """RBF (or linear with order < num_levels) higher orders evaluate forward; their backward raises."""
+    """Orders past the VJP kernel (min(order, num_levels) = 4 here) that are not the exact linear kernel
+    evaluate forward; their backward raises."""
     import gpsig_amd
     X = torch.tensor(golden("linear_chen.npz")["X"][:4].reshape(4, -1), device=DEV, requires_grad=True)
-    for k in (gpsig_amd.SignatureRBF(60, 3, 4, order=2), gpsig_amd.SignatureLinear(60, 3, 4, order=2)):
+    for k in (gpsig_amd.SignatureRBF(60, 3, 5, order=4), gpsig_amd.SignatureLinear(60, 3, 5, order=4)):
         K = k.K(X)
         with pytest.raises(NotImplementedError):
             K.sum().backward()

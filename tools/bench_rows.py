@@ -5,6 +5,10 @@
   C3  PDE signature-kernel Gram K(X), N=1024, L=200, D=5, dyadic=1, solver=1
   C4  inducing-tensor Kuf (K_tens_vs_seq, normalised), T=512 x N=4096, L=100, M=5, increments False/True
   C5  SignatureRBF K(X) normalised, N=8192, L=128, D=8, M=6 on ONE GPU (the 8-GPU config's work)
+  W46, W126  SignatureRBF K(X) normalised at the reference runners' wide channel counts (VERDICT r2 #1:
+      (D+1)*2 = 46 AUSLAN, 126 CMU/KickvsPunch/WalkvsRun): N=1024, L=136 / 128, M=4 (runtime channel loop)
+  P128  PDE Gram K(X) at d = 128 (the VOSF-RNN's num_hidden, train_gpsigrnn_vosf.py:74,82): N=256, L=100,
+      dyadic 1 (increment-tile mode: GEMM of the increments, then the solver)
 
 Per config: whole-call entries/s (median of --reps device-synchronised runs, inputs resident), the
 dominant kernel's launch time from HIP events on its stream, the §8d effective-bandwidth roofline,
@@ -99,11 +103,10 @@ def row_gram(name, n, l, d, m, reps, cpu_s):
                                   sample="4x4-pair raw Gram blocks, oracle/kernels_ref.py fp64 NumPy, 1 process"))
 
 
-def row_pde(reps, cpu_s):
+def row_pde(reps, cpu_s, n=1024, l=200, d=5, dy=1, name="C3"):
     import torch
     from gpsig_amd import ops
     from oracle import pde
-    n, l, d, dy = 1024, 200, 5, 1
     dev = torch.device("cuda", 0)
     Xnp = walks(n, l, d, 0)
     X = torch.as_tensor(Xnp, device=dev)
@@ -117,7 +120,7 @@ def row_pde(reps, cpu_s):
     threads = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16")))
     Xc = Xnp[:16].astype(np.float64)
     cpu = cpu_rate(lambda: pde.pde_gram(Xc[:8], Xc[8:16], dy, 1), 64, cpu_s)
-    return dict(config="C3", workload=f"PDE Gram K(X) N={n} L={l} D={d} dyadic={dy} solver=1 (fp64 solution)",
+    return dict(config=name, workload=f"PDE Gram K(X) N={n} L={l} D={d} dyadic={dy} solver=1 (fp64 solution)",
                 entries_per_s=n * n / t, ms_per_call=t * 1e3, pde_kernel_ms=kms,
                 roofline=dict(bytes_per_entry=b_entry, pairs_per_launch=n * (n + 1) // 2,
                               achieved_GBs=n * (n + 1) / 2 * b_entry / (kms / 1e3) / 1e9,
@@ -176,8 +179,14 @@ def main():
             o = row_gram("C2", 1024, 100, 5, 5, args.reps, args.cpu_seconds)
         elif r == "C5":
             o = row_gram("C5-1gpu", 8192, 128, 8, 6, max(2, args.reps // 2), args.cpu_seconds)
+        elif r == "W46":
+            o = row_gram("W46", 1024, 136, 46, 4, args.reps, args.cpu_seconds)
+        elif r == "W126":
+            o = row_gram("W126", 1024, 128, 126, 4, args.reps, args.cpu_seconds)
         elif r == "C3":
             o = row_pde(args.reps, args.cpu_seconds)
+        elif r == "P128":
+            o = row_pde(args.reps, args.cpu_seconds, n=256, l=100, d=128, dy=1, name="P128")
         elif r in ("C4", "C4i"):
             o = row_kuf(args.reps, args.cpu_seconds, r == "C4i")
         else:
