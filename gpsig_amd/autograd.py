@@ -11,7 +11,11 @@ is the fused Gram kernel and the backward is the gpsig_sig_gram_vjp kernel (gpsi
 
 When a gradient is needed, the forward Gram launch also saves its end-of-sweep state
 (gpsig_sig_gram_state: (M-1)(L2-1) + M floats per pair) and the VJP launch skips its own forward
-sweep; above GRAM_STATE_BYTES (env GPSIG_GRAM_STATE_BYTES) the VJP recomputes it instead.
+sweep; above GRAM_STATE_BYTES (env GPSIG_GRAM_STATE_BYTES) the VJP recomputes it instead.  The Kuf state
+and the PDE fronts work the same way.  All such buffers alive at once (one per autograd node between
+its forward and backward: an SVGP step holds Kuu, Kuf and the Kff diagonal together) share one budget,
+SAVED_STATE_BYTES (env GPSIG_SAVED_STATE_BYTES, default 32 GiB of the 288 GB HBM): a forward that would
+exceed it saves nothing and its backward recomputes.
 
 Gradients reach the sequences (and, through the host-side scaling in kernels.py, the lengthscales)
 and sigma * variances.  Supported for order == 1 (difference True or False); for order > 1 the Gram and
@@ -23,6 +27,8 @@ NotImplementedError on backward.
 from __future__ import annotations
 
 import os
+import threading
+import weakref
 
 import torch
 
@@ -31,6 +37,35 @@ from . import ops
 
 
 GRAM_STATE_BYTES = int(os.environ.get("GPSIG_GRAM_STATE_BYTES", 16 << 30))
+SAVED_STATE_BYTES = int(os.environ.get("GPSIG_SAVED_STATE_BYTES", 32 << 30))
+_saved = {"bytes": 0}
+_saved_lock = threading.Lock()
+
+
+def _release_saved(nbytes):
+    with _saved_lock:
+        _saved["bytes"] -= nbytes
+
+
+def saved_state_bytes() -> int:
+    """Bytes of forward-saved VJP state (Gram state, Kuf state, PDE fronts) currently alive."""
+    return _saved["bytes"]
+
+
+def _saved_buffer(numel: int, device, cap: int):
+    """A float32 buffer for a forward launch's saved VJP state, or None when it is larger than its kind's
+    cap or would take the saved buffers alive at once past SAVED_STATE_BYTES (the backward recomputes).
+    The budget is returned when the buffer is freed (after the backward, or with its autograd node)."""
+    nbytes = numel * 4
+    if numel <= 0 or nbytes > cap:
+        return None
+    with _saved_lock:
+        if _saved["bytes"] + nbytes > SAVED_STATE_BYTES:
+            return None
+        _saved["bytes"] += nbytes
+    t = torch.empty(numel, dtype=torch.float32, device=device)
+    weakref.finalize(t, _release_saved, nbytes)
+    return t
 
 
 def _ho_signature_case(cfg):
@@ -113,8 +148,7 @@ class SigGram(torch.autograd.Function):
         if any(ctx.needs_input_grad[:3]) and cfg["order"] == 1 and cfg["difference"]:
             n2 = None if X2s is None else X2s.shape[0]
             numel = ops.sig_state_numel(Xs.shape[0], n2, Xs.shape[1] if X2s is None else X2s.shape[1], M)
-            if 0 < numel * 4 <= GRAM_STATE_BYTES:
-                state = torch.empty(numel, dtype=torch.float32, device=Xs.device)
+            state = _saved_buffer(numel, Xs.device, GRAM_STATE_BYTES)
         out = ops.sig_gram(Xs.detach(), None if X2s is None else X2s.detach(), M, rs1=rs1, rs2=rs2, scale=sc32,
                            jitter=jit, out_mode=mode, state=state, **kw)
         ctx.state = state
@@ -195,9 +229,12 @@ class TensVsSeq(torch.autograd.Function):
         args = (Zs.detach(), Xs.detach(), cfg["num_levels"], cfg["order"], cfg["base"], cfg["difference"],
                 cfg["increments"])
         numel = ops.tens_state_numel(Zs.shape[1], Xs.shape[0], cfg["num_levels"])
-        if any(ctx.needs_input_grad[:2]) and cfg["order"] == 1 and cfg["difference"] and numel * 4 <= GRAM_STATE_BYTES:
+        st = None
+        if any(ctx.needs_input_grad[:2]) and cfg["order"] == 1 and cfg["difference"]:
+            st = _saved_buffer(numel, Xs.device, GRAM_STATE_BYTES)
+        if st is not None:
             # the training step keeps the forward's end state: the VJP skips its forward sweep
-            out, ctx.state = ops.tens_vs_seq(*args, state=torch.empty(numel, dtype=torch.float32, device=Xs.device))
+            out, ctx.state = ops.tens_vs_seq(*args, state=st)
             return out
         return ops.tens_vs_seq(*args)
 
@@ -240,9 +277,7 @@ def _pde_fronts_buffer(ctx, Xs, npairs, l1, l2, dyadic):
     if not any(ctx.needs_input_grad[:2]):
         return None
     nb = ops.pde_fronts_bytes(npairs, l1, l2, dyadic)
-    if nb == 0 or nb > PDE_FRONTS_BYTES:
-        return None
-    return torch.empty((nb + 3) // 4, dtype=torch.float32, device=Xs.device)
+    return _saved_buffer((nb + 3) // 4, Xs.device, PDE_FRONTS_BYTES) if nb else None
 
 
 class PdeDiag(torch.autograd.Function):
