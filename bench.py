@@ -303,6 +303,10 @@ def main():
                    "global_batch": n, "seq_len": l, "parallelism": f"row-shard{world}" if world > 1 else "single"},
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                     # frac is an effective-bandwidth ratio (SURVEY.md 8d's algorithmic bytes of the
+                     # materialised-tile design / HBM peak); the fused kernel's physical limiter is VALU
+                     # issue, whose busy fraction from the PMC profile is valu_busy below
+                     "frac_kind": "effective-bandwidth (algorithmic bytes / HBM peak)",
                      "kernel": "sig_fo_kernel", "seed_engine": args.seed_engine, "gram_path": args.gram_path,
                      "launch_ms": avg_launch_s * 1e3, "bytes_per_entry": b_entry,
                      "entries_per_launch": entries_per_launch,

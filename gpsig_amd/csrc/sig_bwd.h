@@ -18,9 +18,12 @@
 //       gradients: x-rows are reduced across the wave and added to gX, y-columns accumulate in lane
 //       registers and are added to gY at the end.
 //
-// Both sweeps evaluate each k(x_i, y_j) row with the same instructions (one exp per cell), so the
-// cells dM of the reverse sweep are bitwise those of the forward sweep and the inversion only carries
-// the fp32 rounding of the forward sums.
+// The cells the reverse sweep inverts with are not bitwise those its forward state came from: the RBF
+// difference seed regenerates them in chunks of RC rows with exp-free recurrences (chain over the lane's
+// W columns, exact row every RC rows), while the forward sweep here evaluates k directly and the forward
+// launch that saves the state (sig_fo.h, RbfSeedPk) chains column pairs (w, w + W/2) and re-anchors
+// every 32 rows.  The cells agree to ~1e-7 relative, so the recovered state carries that plus the fp32
+// rounding of the sums (gradient error <= 6e-6 norm-relative vs fp64 autodiff).
 #pragma once
 #include "sig_common.h"
 
@@ -727,8 +730,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
 
     if constexpr (RBF && DIFF) {
       // Chunked: the cells of RC rows are regenerated forward from an exact row (k and expm1(q) from
-      // x - y) with the exp-free recurrences of the forward kernel (sig_common.h RbfSeedPk; chunk
-      // starts at multiples of RC <= its anchor period, so the cells are the forward launch's) into
+      // x - y) with exp-free recurrences like the forward kernel's (sig_common.h RbfSeedPk: the same
+      // cells up to the rounding of the recurrences, whose chain order and anchor rows differ) into
       // this lane's LDS slots, then consumed in reverse.  Cells with |p| or |c| >= EM1_TAU take the
       // corner difference of the k grid with an exact next row (wave-uniform branch).
       float(*cb)[64][2 * W] = cbuf[wave];
