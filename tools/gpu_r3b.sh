@@ -1,11 +1,12 @@
-# Round-3 measurements on one MI355X: headline bench + its kernel trace, the SURVEY 8 rows (with the
-# wide-channel rows), the gradient paths, and one SQ counter pass of the wide-channel Gram row.
+# Round-3 measurements on one MI355X: the PDE parity tests (lane-group geometry change), the headline
+# bench + its kernel trace, the SURVEY 8 rows (with the wide-channel rows), the gradient paths, and one
+# SQ counter pass of the wide-channel Gram row.
 set -o pipefail
 export TMPDIR=/tmp
 O=gpurun_out/r3b
 mkdir -p $O
-timeout -k 10 300 python3 -u bench.py --steps 10 --warmup 3 > $O/bench.json 2> $O/bench.err || exit 1
-cat $O/bench.json
+timeout -k 10 300 python -u -m pytest tests/test_pde_gpu.py tests/test_pde_grad.py tests/test_pde_wide_gpu.py -q --timeout 200 --timeout-method thread -p no:cacheprovider > $O/pde_tests.log 2>&1
+r=$?; tail -3 $O/pde_tests.log; [ $r -ne 0 ] && [ $r -ne 1 ] && exit $r
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $O/trace -o run --output-format csv -- python3 bench.py --steps 5 --warmup 2 --no-cpu --no-check --no-probe > $O/trace.log 2>&1 || exit 2
 timeout -k 10 600 python3 -u tools/bench_rows.py --rows C2,C3,C4,C4i,C5,W46,W126,P128 --out $O/rows.json > $O/rows.log 2>&1 || exit 3
 cat $O/rows.log
