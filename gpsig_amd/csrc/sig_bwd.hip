@@ -5,13 +5,22 @@
 
 namespace gpsig {
 int features(const float *X, int n, int l, int d, int DP, float *F, hipStream_t s);
-int fo_fixed_max();
 size_t sig_bwd_wide_workspace(int n1, int l1, int n2, int l2, int d);
 int sig_bwd_wide(BwdArgs a, const float *X, const float *Y, int seed, void *workspace, size_t workspace_bytes,
                  hipStream_t s, int order = 1);
 bool ho_bwd_supported(int l2, int order, int M, int seed);
-// channel counts past the VJP's instantiations (or past the forward's crossover): the wide-channel VJP
-static bool bwd_wide(int d) { return d > 16 || d > fo_fixed_max(); }
+// channel counts past the VJP's instantiations: the wide-channel VJP (point-weight tiles + GEMMs; slower
+// than the register form at few channels: d = 5 69.7 vs 31.8 ms fwd+bwd at N = 1024, L = 100).
+// GPSIG_VJP_FIXED_MAX lowers the crossover for A/B runs.
+static int vjp_fixed_max() {
+  static const int v = [] {
+    const char *e = getenv("GPSIG_VJP_FIXED_MAX");
+    const int x = e ? atoi(e) : 16;
+    return x < 16 ? (x < 0 ? 0 : x) : 16;
+  }();
+  return v;
+}
+static bool bwd_wide(int d) { return d > vjp_fixed_max(); }
 template <int DP, int M>
 int sig_bwd_launch_dpm(const BwdArgs &a, int seed, long long nblocks, hipStream_t s);
 

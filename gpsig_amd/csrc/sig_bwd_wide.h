@@ -20,15 +20,16 @@
 
 namespace gpsig {
 
-#ifndef GPSIG_WIDE_R
-#define GPSIG_WIDE_R 4
+// rows per regenerated chunk of the VJPs (LDS: 4 waves x RC x 64 lanes x 2W floats)
+#ifndef GPSIG_WIDE_BWD_R
+#define GPSIG_WIDE_BWD_R 4
 #endif
 
 template <int W, int LP, int M, int SEED>
 __global__ __launch_bounds__(256) void sig_bwd_wide_kernel(BwdArgs p) {
   constexpr int G = 64 / LP;
   constexpr int W2 = W / 2;
-  constexpr int RC = GPSIG_WIDE_R;
+  constexpr int RC = GPSIG_WIDE_BWD_R;
   constexpr bool DIFF = (SEED == SEED_RBF_DIFF || SEED == SEED_LIN_DIFF);
   constexpr bool RBF = (SEED == SEED_RBF_DIFF || SEED == SEED_RBF_POINT);
   constexpr int ML = M > 1 ? M - 1 : 1;

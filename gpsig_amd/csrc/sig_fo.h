@@ -19,9 +19,12 @@
 
 namespace gpsig {
 
-// Rows per channel-loop chunk of the wide-channel seeds (DP == 0, wide.h)
+// Rows per channel-loop chunk of the wide-channel seeds (DP == 0, wide.h): each channel's y columns are
+// loaded once per chunk, so the loop's loads per FMA fall as 1/R.  Measured (N = 1024, L = 128, M = 4,
+// tools/ab_wide_r.sh): R = 4 -> 8 takes D = 46 from 56.9 to 32.5 ms and D = 126 from 153.6 to 83.6 ms
+// (251 VGPRs, 2 waves/SIMD; the loop was load-bound, VALU busy 0.21 at R = 4).
 #ifndef GPSIG_WIDE_R
-#define GPSIG_WIDE_R 4
+#define GPSIG_WIDE_R 8
 #endif
 constexpr int WIDE_R = GPSIG_WIDE_R;
 

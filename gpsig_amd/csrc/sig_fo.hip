@@ -86,7 +86,7 @@ int sig_fo_launch(const SigArgs &a0, int DP, int seed, long long nblocks, hipStr
   switch (DP) {
 #define CASE(v) \
   case v: return fo_dp<v>(a, seed, nblocks, s);
-    CASE(0) CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(8) CASE(16) CASE(32)
+    CASE(0) CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(8)
 #undef CASE
     default: return GPSIG_EUNSUPPORTED;
   }

@@ -27,8 +27,8 @@
 
 namespace gpsig {
 
-#ifndef GPSIG_WIDE_R
-#define GPSIG_WIDE_R 4
+#ifndef GPSIG_WIDE_BWD_R
+#define GPSIG_WIDE_BWD_R 4
 #endif
 
 // f(std::integral_constant<int, k>) for k = B .. E-1 (ascending) / E-1 .. B (descending)
@@ -74,7 +74,7 @@ constexpr size_t ho_bwd_lds_bytes() {
 template <int ORD, int M, int SEED>
 __global__ __launch_bounds__(256) void sig_ho_bwd_kernel(BwdArgs p) {
   constexpr int W = 4, W2 = 2;
-  constexpr int RC = GPSIG_WIDE_R;
+  constexpr int RC = GPSIG_WIDE_BWD_R;
   constexpr bool RBF = SEED == SEED_RBF_DIFF;
   static_assert(SEED == SEED_RBF_DIFF || SEED == SEED_LIN_DIFF, "higher order: difference seeds");
   static_assert(M >= 2 && ORD >= 2 && ORD <= M, "higher order");

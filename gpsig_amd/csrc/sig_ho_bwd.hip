@@ -5,7 +5,7 @@
 
 namespace gpsig {
 
-constexpr size_t HO_BWD_STATIC_LDS = (size_t)4 * GPSIG_WIDE_R * 64 * 8 * sizeof(float);  // cbuf
+constexpr size_t HO_BWD_STATIC_LDS = (size_t)4 * GPSIG_WIDE_BWD_R * 64 * 8 * sizeof(float);  // cbuf
 
 template <int ORD, int M>
 static int launch_ho_bwd(const BwdArgs &a, int seed, long long nblocks, hipStream_t s) {

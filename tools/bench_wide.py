@@ -50,7 +50,7 @@ def main():
         cells = pairs * (args.l - 1) ** 2
         B = 4 * (args.l - 1) ** 2 + 4 * (args.m + 1)
         print(json.dumps({"n": args.n, "l": args.l, "d": d, "m": args.m,
-                          "fixed_max": os.environ.get("GPSIG_FO_FIXED_MAX", "32"), "ms": round(ms, 3),
+                          "fixed_max": os.environ.get("GPSIG_FO_FIXED_MAX", "8"), "ms": round(ms, 3),
                           "cells_per_s": cells / (ms * 1e-3), "frac_8d": pairs * B / (ms * 1e-3) / 8e12,
                           "dot_tflops": cells * 1.25 * d * 2 / (ms * 1e-3) / 1e12}), flush=True)
 

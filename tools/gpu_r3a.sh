@@ -7,5 +7,5 @@ timeout -k 10 300 python -u tools/bench_wide.py --d 8 16 32 46 126 > gpurun_out/
 GPSIG_FO_FIXED_MAX=0 timeout -k 10 300 python -u tools/bench_wide.py --d 5 8 16 32 > gpurun_out/r3a/wide_forced.jsonl 2>&1 || exit $?
 cat gpurun_out/r3a/wide.jsonl gpurun_out/r3a/wide_forced.jsonl
 timeout -k 10 300 python -u tools/bench_grad.py --only gram > gpurun_out/r3a/grad_fixed.jsonl 2>&1 || exit $?
-GPSIG_FO_FIXED_MAX=0 timeout -k 10 300 python -u tools/bench_grad.py --only gram > gpurun_out/r3a/grad_wide.jsonl 2>&1 || exit $?
+GPSIG_VJP_FIXED_MAX=0 timeout -k 10 300 python -u tools/bench_grad.py --only gram > gpurun_out/r3a/grad_wide.jsonl 2>&1 || exit $?
 cat gpurun_out/r3a/grad_fixed.jsonl gpurun_out/r3a/grad_wide.jsonl
