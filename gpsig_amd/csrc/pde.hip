@@ -402,6 +402,9 @@ static int launch_pde_rep(const PdeArgs &a, long long nblocks, hipStream_t s) {
 // the one-pair-per-wave
 // geometry of pde_rep_w wins.  GPSIG_PDE_LP = 16 / 32 / 64 pins the lane group (A/B).
 struct PdeLp { int LP, W; };
+// register budget of a lane group's coarse increments: (W / REP) * DP floats; W = 26 (C3: 16 x 26 = 416
+// columns for 398, four pairs per wave) fits 13 x 5 at 194 VGPRs
+constexpr int pde_lp_regs(int W) { return W == 26 ? 65 : 64; }
 inline double pde_cost(int IC, int J, int REP, int DP, int W, int G) {
   const int U = (J + W - 1) / W;
   return (double)(IC + U - 1) * (3.0 * REP * W + (DP / 2.0 + 7.0) * W / REP + 2.0 * REP + 12.0) / G;
@@ -418,8 +421,9 @@ inline PdeLp pde_pick_lp(int IC, int J, int REP, int DP) {
   if (force == 64) return best;
   double bc = pde_cost(IC, J, REP, DP, pde_w64(J, REP), 1);
   for (int LP : {16, 32})
-    for (int W : {8, 14, 16, 24}) {
-      if (W % REP || LP * W < J || (W / REP) * DP > 64) continue;
+    for (int W : {8, 14, 16, 24, 26}) {
+      if (W % REP || LP * W < J || (W / REP) * DP > pde_lp_regs(W)) continue;
+      if (W == 26 && LP != 16) continue;
       if (force && force != LP) continue;
       const double c = pde_cost(IC, J, REP, DP, W, 64 / LP);
       if (force ? (best.LP == 64 || c < bc) : c < bc) { bc = c; best = {LP, W}; }
@@ -429,7 +433,7 @@ inline PdeLp pde_pick_lp(int IC, int J, int REP, int DP) {
 
 template <typename T, int DP, int W, int REP, int LP>
 static int launch_pde_lp(const PdeArgs &a, long long nblocks, hipStream_t s) {
-  if constexpr (W % REP != 0 || (W / REP) * DP > 64) {
+  if constexpr (W % REP != 0 || (W / REP) * DP > pde_lp_regs(W)) {
     return GPSIG_EUNSUPPORTED;
   } else {
     const size_t lds = ((size_t)4 * (a.l1 - 1) * DP + 3) / 4 * 4 * sizeof(float);
@@ -443,7 +447,7 @@ template <typename T, int DP, int REP>
 static int pde_lp_dispatch(const PdeArgs &a, long long nblocks, PdeLp g, hipStream_t s) {
 #define GPSIG_LPW(lp, w) \
   if (g.LP == lp && g.W == w) return launch_pde_lp<T, DP, w, REP, lp>(a, nblocks, s);
-  GPSIG_LPW(16, 8) GPSIG_LPW(16, 14) GPSIG_LPW(16, 16) GPSIG_LPW(16, 24)
+  GPSIG_LPW(16, 8) GPSIG_LPW(16, 14) GPSIG_LPW(16, 16) GPSIG_LPW(16, 24) GPSIG_LPW(16, 26)
   GPSIG_LPW(32, 8) GPSIG_LPW(32, 14) GPSIG_LPW(32, 16) GPSIG_LPW(32, 24)
 #undef GPSIG_LPW
   return GPSIG_EUNSUPPORTED;
