@@ -45,6 +45,7 @@ _SZ = ctypes.c_size_t
 
 SIGNATURES = {
     "gpsig_sig_workspace_bytes": (_SZ, [_I, _I, _I, _I, _I]),
+    "gpsig_sig_workspace_bytes_ex": (_SZ, [_I, _I, _I, _I, _I, _I, _I]),
     "gpsig_sig_split_bytes": (_SZ, [_I, _I, _I, _I]),
     "gpsig_sig_vjp_workspace_bytes": (_SZ, [_I, _I, _I, _I, _I, _I, _I]),
     "gpsig_sig_gram": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _I, _I,

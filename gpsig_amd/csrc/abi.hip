@@ -11,6 +11,10 @@ int sig_fo_launch(const SigArgs &a, int DP, int seed, long long nblocks, hipStre
 int fo_lanes_per_pair(int l2, int DP, int M, bool mf, int seed);
 size_t fo_split_bytes(int l1, int l2, int DP, int M);
 int sig_ho_launch(const SigArgs &a, int DP, int seed, long long nblocks, hipStream_t s);
+bool ho_tiled(int d, int order);
+size_t ho_tile_bytes(int n1, int l1, int n2, int l2, int d, int pair_mode);
+int sig_ho_tiled(SigArgs a, const float *X, const float *Y, int d, void *workspace, size_t workspace_bytes,
+                 hipStream_t s);
 int ho_lanes_per_pair(int l2, int order, int M);
 int pde_launch(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int dyadic, int solver,
                int pair_mode, int row_begin, int row_end, float *out, int out_row0, int out_rows,
@@ -72,6 +76,14 @@ extern "C" size_t gpsig_sig_workspace_bytes(int n1, int l1, int n2, int l2, int 
   return feat_bytes(n1, l1, d) + feat_bytes(n2, l2, d);
 }
 
+// The workspace of one gpsig_sig_gram / gpsig_sig_diag call: the feature records, or for the higher-order
+// recursion past 32 channels the increments and one chunk's increment tile (sig_ho.hip tile mode).
+extern "C" size_t gpsig_sig_workspace_bytes_ex(int n1, int l1, int n2, int l2, int d, int order, int pair_mode) {
+  if (n1 <= 0 || n2 <= 0 || l1 < 1 || l2 < 1 || d <= 0) return 0;
+  if (ho_tiled(d, order) && l1 >= 2 && l2 >= 2) return ho_tile_bytes(n1, l1, n2, l2, d, pair_mode);
+  return gpsig_sig_workspace_bytes(n1, l1, n2, l2, d);
+}
+
 extern "C" size_t gpsig_sig_split_bytes(int l1, int l2, int d, int num_levels) {
   const int DP = pad_channels(d, 1);
   if (DP == 0 || l1 < 2 || l2 < 2 || num_levels < 1 || num_levels > 8) return 0;
@@ -102,11 +114,31 @@ static int sig_gram_impl(const float *X, int n1, int l1, const float *Y, int n2,
   if (mfma && (seed != SEED_RBF_DIFF || order != 1 || state)) return GPSIG_EUNSUPPORTED;
   if (split && (mfma || seed != SEED_RBF_DIFF || order != 1 || state || pair_mode == GPSIG_PAIRS_DIAG))
     return GPSIG_EUNSUPPORTED;
+  const bool tiled = ho_tiled(d, order);  // higher order past 32 channels: cells from an increment-Gram tile
+  if (tiled && (seed != SEED_LIN_DIFF || mfma || split || state)) return GPSIG_EUNSUPPORTED;
   const bool wide = wide_channels(d, order);
-  const int DP = wide ? 0 : pad_channels(d, order);
-  if (seed < 0 || (DP == 0 && !wide)) return GPSIG_EUNSUPPORTED;
+  const int DP = (wide || tiled) ? 0 : pad_channels(d, order);
+  if (seed < 0 || (DP == 0 && !wide && !tiled)) return GPSIG_EUNSUPPORTED;
   if (wide && (mfma || split)) return GPSIG_EUNSUPPORTED;
   if (row_end == row_begin) return GPSIG_OK;
+  if (tiled) {
+    SigArgs a{};
+    a.n1 = n1; a.l1 = l1; a.n2 = n2; a.l2 = l2;
+    a.M = num_levels;
+    a.order = order;
+    a.pair_mode = pair_mode;
+    a.row_begin = row_begin;
+    a.row_end = row_end;
+    a.rs1 = rs1; a.rs2 = rs2; a.scale = scale;
+    a.jitter = jitter;
+    a.out_mode = out_mode;
+    a.out = out;
+    a.out_row0 = out_row0;
+    a.out_rows = out_rows;
+    a.out_ld = n2;
+    a.out_lvl = pair_mode == GPSIG_PAIRS_DIAG ? (long long)n1 : (long long)out_rows * n2;
+    return sig_ho_tiled(a, X, Y, d, workspace, workspace_bytes, s);
+  }
 
   const bool same = (X == Y && n1 == n2 && l1 == l2);
   const size_t fx_b = wide ? feat_bytes(n1, l1, d) : align256((size_t)n1 * l1 * feat_stride(DP) * sizeof(float));

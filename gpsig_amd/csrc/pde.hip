@@ -591,8 +591,9 @@ int increments_launch(const float *X, int n, int l, int d, float *dX, hipStream_
 static size_t al256p(size_t b) { return (b + 255) & ~(size_t)255; }
 constexpr size_t PDE_TILE_BYTES = (size_t)1 << 30;  // increment tile of one chunk of x-rows
 
-// x-rows per chunk of the tiled path (a multiple of 4) and the tile's row length
-static void pde_tile_chunk(int n1, int l1, int n2, int l2, int pair_mode, int &rows, long long &cols) {
+// x-rows per chunk of the tiled paths (a multiple of 4) and the tile's row length (also the higher-order
+// Gram's tile mode, sig_ho.hip)
+void pde_tile_chunk(int n1, int l1, int n2, int l2, int pair_mode, int &rows, long long &cols) {
   cols = pair_mode == GPSIG_PAIRS_DIAG ? (long long)(l1 - 1) : (long long)n2 * (l2 - 1);
   long long r = (long long)(PDE_TILE_BYTES / ((size_t)(l1 - 1) * cols * sizeof(float)));
   r = r < 4 ? 4 : (r / 4) * 4;

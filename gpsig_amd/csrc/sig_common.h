@@ -46,6 +46,13 @@ struct SigArgs {
   // record strides (floats) of X and Y
   int wd, lw1, lw2;
   long long sx, sy;
+  // higher order past the fixed channel counts (linear base kernel, sig_ho.hip): the cells of pair
+  // (a, b), row i, column j at tile + (a - tile_a0) tile_as + (b - tile_b0) (l2 - 1) + i tile_ld + j (DIAG:
+  // without the b term), a GEMM of the increments; RX / RY the raw (n, l, wd) inputs (level 1 closed form)
+  const float *tile;
+  long long tile_as, tile_ld;
+  int tile_a0, tile_b0;
+  const float *RX, *RY;
 };
 
 // Saved forward state of a first-order pair (gpsig_sig_gram_state): column sums of levels 1..M-1

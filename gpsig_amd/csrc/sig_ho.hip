@@ -62,11 +62,15 @@ GPSIG_DEV void excl_scan_cols(const float (&v)[W], float (&out)[W], float *cr, i
   for (int w = 1; w < W; ++w) out[w] = base + t[w - 1];
 }
 
-template <int DP, int W, int ORD, int MMAX, int SEED>
+// TILE (linear base kernel, any channel count): the cells come from the increment-Gram tile of the
+// launch (SigArgs::tile, a GEMM of the increments, the reference's own tf.matmul of the linear base
+// kernel, kernels.py:1042-1044), DP is unused.
+template <int DP, int W, int ORD, int MMAX, int SEED, bool TILE = false>
 __global__ __launch_bounds__(256) void sig_ho_kernel(SigArgs p) {
   using Seed = RowSeed<DP, W, SEED>;
   using Lay = HoLayout<ORD, MMAX>;
   constexpr int FS = feat_stride(DP);
+  static_assert(!TILE || SEED == SEED_LIN_DIFF, "tile cells: linear difference seed");
   const int lane = threadIdx.x & 63;
   const int wave = wave_uniform(threadIdx.x >> 6);
 
@@ -93,8 +97,12 @@ __global__ __launch_bounds__(256) void sig_ho_kernel(SigArgs p) {
   if (p.pair_mode == GPSIG_PAIRS_UPPER) pair_ok = pair_ok && b >= a;
   if (!pair_ok) return;  // one pair per wave: wave-uniform
 
-  const float *__restrict__ fx = p.FX + (long long)a * p.l1 * FS;
-  const float *__restrict__ fy = p.FY + (long long)b * p.l2 * FS;
+  const float *__restrict__ fx = TILE ? nullptr : p.FX + (long long)a * p.l1 * FS;
+  const float *__restrict__ fy = TILE ? nullptr : p.FY + (long long)b * p.l2 * FS;
+  const float *__restrict__ tcells =
+      TILE ? p.tile + (long long)(a - p.tile_a0) * p.tile_as +
+                 (p.pair_mode == GPSIG_PAIRS_DIAG ? 0 : (long long)(b - p.tile_b0) * (p.l2 - 1))
+           : nullptr;
   const int M = p.M;
   const int nrows = Seed::DIFF ? p.l1 - 1 : p.l1;
   constexpr int CPB = 64 * W - 1;
@@ -110,7 +118,11 @@ __global__ __launch_bounds__(256) void sig_ho_kernel(SigArgs p) {
   for (int blk = 0; blk < nblk; ++blk) {
   const int j0 = blk * CPB;
   Seed seed;
-  seed.init(fx, fy + (long long)j0 * FS, lane, nblk == 1 ? p.l2 : min(p.l2 - j0, CPB + 1));
+  if constexpr (!TILE) seed.init(fx, fy + (long long)j0 * FS, lane, nblk == 1 ? p.l2 : min(p.l2 - j0, CPB + 1));
+  // TILE: this lane's cell columns of the block (the halo column of a block is not a cell of it)
+  bool tcol[W];
+#pragma unroll
+  for (int w = 0; w < W; ++w) tcol[w] = lane * W + w < CPB && j0 + lane * W + w < p.l2 - 1;
 
   float CB[Lay::total][W];
 #pragma unroll
@@ -119,13 +131,19 @@ __global__ __launch_bounds__(256) void sig_ho_kernel(SigArgs p) {
     for (int w = 0; w < W; ++w) CB[k][w] = 0.0f;
 
   RowData<DP> rd;
-  rd.load(fx, 0, SEED);
+  if constexpr (!TILE) rd.load(fx, 0, SEED);
   for (int i = 0; i < nrows; ++i) {
     float *__restrict__ cr = carry + (long long)i * ncar;
     RowData<DP> rn;
-    rn.load(fx, i + 1 < nrows ? i + 1 : i, SEED);
     float dM[W];
-    seed.template row<true>(rd, dM);
+    if constexpr (TILE) {
+      const float *__restrict__ tr = tcells + (long long)i * p.tile_ld + j0 + lane * W;
+#pragma unroll
+      for (int w = 0; w < W; ++w) dM[w] = tcol[w] ? tr[w] : 0.0f;
+    } else {
+      rn.load(fx, i + 1 < nrows ? i + 1 : i, SEED);
+      seed.template row<true>(rd, dM);
+    }
 
     float R[ORD][ORD][W];
 #pragma unroll
@@ -206,7 +224,7 @@ __global__ __launch_bounds__(256) void sig_ho_kernel(SigArgs p) {
             for (int w = 0; w < W; ++w) CB[Lay::off(m) + x][w] += colsum[x][w];
       }
     }
-    rd = rn;
+    if constexpr (!TILE) rd = rn;
   }
 
 #pragma unroll
@@ -224,8 +242,18 @@ __global__ __launch_bounds__(256) void sig_ho_kernel(SigArgs p) {
   K[0] = 1.0f;
 #pragma unroll
   for (int m = 1; m <= MMAX; ++m) K[m] = Kacc[m];
+  if constexpr (TILE) {
+    // level 1 in closed form, sum_ij <dx_i, dy_j> = <x_L - x_0, y_L - y_0> (fp64, channels over the lanes)
+    const int d = p.wd;
+    const float *xa = p.RX + (long long)a * p.l1 * d, *yb = p.RY + (long long)b * p.l2 * d;
+    double s = 0.0;
+    for (int k = lane; k < d; k += 64)
+      s += ((double)xa[(long long)(p.l1 - 1) * d + k] - (double)xa[k]) * ((double)yb[(long long)(p.l2 - 1) * d + k] - (double)yb[k]);
+    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
+    K[1] = (float)s;
+  }
   if (lane == 0) {
-    K[1] = level1_closed<DP, SEED>(fx, fy, p.l1, p.l2);  // ho seeds are the DIFF seeds
+    if constexpr (!TILE) K[1] = level1_closed<DP, SEED>(fx, fy, p.l1, p.l2);  // ho seeds are the DIFF seeds
     store_pair<MMAX>(p, a, b, K);
   }
 }
@@ -246,31 +274,31 @@ static size_t ho_carry_bytes(int l1, int order, int M, int nblk) {
 }
 constexpr size_t HO_MAX_CARRY_BYTES = 160 * 1024;
 
-template <int DP, int W, int ORD, int SEED>
+template <int DP, int W, int ORD, int SEED, bool TILE = false>
 static int launch_ho(const SigArgs &a0, long long nblocks, hipStream_t s) {
   if (nblocks <= 0) return GPSIG_OK;
   SigArgs a = a0;
   a.nblk = ho_blocks(a.l2, W);
   const size_t lds = ho_carry_bytes(a.l1, ORD, a.M, a.nblk);
   if (lds > HO_MAX_CARRY_BYTES) return GPSIG_EUNSUPPORTED;
-  hipLaunchKernelGGL((sig_ho_kernel<DP, W, ORD, 8, SEED>), dim3((unsigned)nblocks), dim3(256), lds, s, a);
+  hipLaunchKernelGGL((sig_ho_kernel<DP, W, ORD, 8, SEED, TILE>), dim3((unsigned)nblocks), dim3(256), lds, s, a);
   return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
 }
 
 int ho_lanes_per_pair(int l2, int order, int M) { return (M <= 8 && order <= 8 && l2 >= 2) ? 64 : 0; }
 
-template <int DP, int SEED>
+template <int DP, int SEED, bool TILE = false>
 static int ho_dispatch(const SigArgs &a, long long nblocks, hipStream_t s) {
   const int W = ho_w(a.l2, a.order);
   switch (a.order) {
 #define ORDCASE(o)                                                          \
   case o:                                                                   \
-    if (W == 1) return launch_ho<DP, 1, o, SEED>(a, nblocks, s);            \
+    if (W == 1) return launch_ho<DP, 1, o, SEED, TILE>(a, nblocks, s);      \
     if constexpr (o <= 5) {                                                 \
-      if (W == 2) return launch_ho<DP, 2, o, SEED>(a, nblocks, s);          \
+      if (W == 2) return launch_ho<DP, 2, o, SEED, TILE>(a, nblocks, s);    \
     }                                                                       \
     if constexpr (o <= 4) {                                                 \
-      if (W == 4) return launch_ho<DP, 4, o, SEED>(a, nblocks, s);          \
+      if (W == 4) return launch_ho<DP, 4, o, SEED, TILE>(a, nblocks, s);    \
     }                                                                       \
     return GPSIG_EUNSUPPORTED;
     ORDCASE(2) ORDCASE(3) ORDCASE(4) ORDCASE(5) ORDCASE(6) ORDCASE(7) ORDCASE(8)
@@ -291,6 +319,92 @@ int sig_ho_launch(const SigArgs &a, int DP, int seed, long long nblocks, hipStre
 #undef DCASE
     default: return GPSIG_EUNSUPPORTED;
   }
+}
+
+// ---- tile mode: the higher-order Gram past the fixed channel counts (linear base kernel, difference)
+void pde_tile_chunk(int n1, int l1, int n2, int l2, int pair_mode, int &rows, long long &cols);
+size_t pde_tile_scratch_bytes(int n1, int l1, int n2, int l2, int d, int pair_mode);
+int increments_launch(const float *X, int n, int l, int d, float *dX, hipStream_t s);
+int gemm_f32(hipStream_t s, bool transA, bool transB, int M, int N, int K, float alpha, const float *A, long long lda,
+             long long sA, const float *B, long long ldb, long long sB, float beta, float *C, long long ldc,
+             long long sC, int batch, int skip_rb, int skip_cb, float *partial);
+
+bool ho_tiled(int d, int order) { return order > 1 && d > 32; }
+size_t ho_tile_bytes(int n1, int l1, int n2, int l2, int d, int pair_mode) {
+  return pde_tile_scratch_bytes(n1, l1, n2, l2, d, pair_mode);
+}
+static inline long long ho_upper_prefix(long long r, long long ntb) { return r * ntb - 4 * r * (r - 1) / 2; }
+
+// Chunks of x-rows: the increment tile of the chunk (one matrix-core GEMM dX_chunk dY^T, batched per pair
+// for DIAG), then the tile-fed recursion.  a: filled by the caller (rows, mode, output, M, order).
+int sig_ho_tiled(SigArgs a, const float *X, const float *Y, int d, void *workspace, size_t workspace_bytes,
+                 hipStream_t s) {
+  const int n1 = a.n1, l1 = a.l1, n2 = a.n2, l2 = a.l2, pm = a.pair_mode;
+  const int IC = l1 - 1, JC = l2 - 1;
+  if (a.M > 8 || a.order > 8) return GPSIG_EUNSUPPORTED;
+  if (!workspace || workspace_bytes < ho_tile_bytes(n1, l1, n2, l2, d, pm)) return GPSIG_EWORKSPACE;
+  int rows;
+  long long cols;
+  pde_tile_chunk(n1, l1, n2, l2, pm, rows, cols);
+  char *w = static_cast<char *>(workspace);
+  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+  float *dX = reinterpret_cast<float *>(w);
+  w += al((size_t)n1 * IC * d * sizeof(float));
+  float *dY = dX;
+  if (pm == GPSIG_PAIRS_RECT) {
+    dY = reinterpret_cast<float *>(w);
+    w += al((size_t)n2 * JC * d * sizeof(float));
+  }
+  float *T = reinterpret_cast<float *>(w);
+  int rc = increments_launch(X, n1, l1, d, dX, s);
+  if (rc) return rc;
+  if (pm == GPSIG_PAIRS_RECT && (rc = increments_launch(Y, n2, l2, d, dY, s))) return rc;
+  a.tile = T;
+  a.RX = X;
+  a.RY = pm == GPSIG_PAIRS_RECT ? Y : X;
+  a.wd = d;
+  const int rb0 = a.row_begin, rb1 = a.row_end;
+  for (int r0 = (rb0 / 4) * 4; r0 < rb1; r0 += rows) {
+    const int r1 = r0 + rows < rb1 ? r0 + rows : rb1;
+    const int c0 = r0 > rb0 ? r0 : rb0;
+    SigArgs c = a;
+    c.row_begin = c0;
+    c.row_end = r1;
+    long long nblocks;
+    if (pm == GPSIG_PAIRS_DIAG) {
+      c.tile_a0 = c0;
+      c.tile_b0 = 0;
+      c.tile_as = (long long)IC * IC;
+      c.tile_ld = IC;
+      nblocks = (r1 - c0 + 3) / 4;
+      rc = gemm_f32(s, false, true, IC, IC, d, 1.0f, dX + (long long)c0 * IC * d, d, (long long)IC * d,
+                    dX + (long long)c0 * IC * d, d, (long long)IC * d, 0.0f, T, IC, (long long)IC * IC, r1 - c0, 0, 0,
+                    nullptr);
+    } else {
+      const int b0 = pm == GPSIG_PAIRS_UPPER ? r0 : 0;
+      const long long tc = (long long)(n2 - b0) * JC;
+      c.tile_a0 = r0;
+      c.tile_b0 = b0;
+      c.tile_as = (long long)IC * tc;
+      c.tile_ld = tc;
+      const int ta0 = r0 / 4, ta1 = (r1 + 3) / 4;
+      c.tiles_a0 = ta0;
+      c.ntb = n2;  // one pair per wave: b-tiles are single sequences
+      if (pm == GPSIG_PAIRS_RECT) {
+        nblocks = (long long)(ta1 - ta0) * n2;
+      } else {
+        c.tile_base = ho_upper_prefix(ta0, n2);
+        nblocks = ho_upper_prefix(ta1, n2) - c.tile_base;
+      }
+      rc = gemm_f32(s, false, true, (r1 - r0) * IC, (int)tc, d, 1.0f, dX + (long long)r0 * IC * d, d, 0,
+                    dY + (long long)b0 * JC * d, d, 0, 0.0f, T, tc, 0, 1, pm == GPSIG_PAIRS_UPPER ? IC : 0,
+                    pm == GPSIG_PAIRS_UPPER ? JC : 0, nullptr);
+    }
+    if (rc) return rc;
+    if (nblocks > 0x7fffffffLL) return GPSIG_EUNSUPPORTED;
+    if ((rc = ho_dispatch<1, SEED_LIN_DIFF, true>(c, nblocks, s))) return rc;
+  }
+  return GPSIG_OK;
 }
 
 }  // namespace gpsig

@@ -128,7 +128,7 @@ def sig_diag(X: torch.Tensor, num_levels: int, order: int = 1, base="rbf", diffe
             out[m] = (S[:, off:off + w] ** 2).sum(1)
             off += w
         return torch.rsqrt(out + float(jitter)) if rsqrt else out
-    nb = lib.gpsig_sig_workspace_bytes(n, l, n, l, d)
+    nb = lib.gpsig_sig_workspace_bytes_ex(n, l, n, l, d, order, L.PAIRS_DIAG)
     ws = workspace(X.device, nb)
     rc = lib.gpsig_sig_diag(X.data_ptr(), n, l, d, num_levels, order, base_kind(base), int(difference), float(jitter),
                             L.OUT_RSQRT if rsqrt else L.OUT_LEVELS, out.data_ptr(), ws.data_ptr(), ws.numel(),
@@ -191,11 +191,11 @@ def sig_gram(X: torch.Tensor, Y: torch.Tensor | None, num_levels: int, order: in
         rs1, rs2 = _f32(rs1), _f32(rs2)
     if scale is not None:
         scale = _f32(scale)
-    nb = lib.gpsig_sig_workspace_bytes(n1, l1, n2, l2, d)
+    pm = L.PAIRS_UPPER if sym else L.PAIRS_RECT
+    nb = lib.gpsig_sig_workspace_bytes_ex(n1, l1, n2, l2, d, order, pm)
     if base_kind(base) & L.GRAM_SPLIT:  # split diagnostic: one chunk of pairs' cells in the workspace
         nb += lib.gpsig_sig_split_bytes(l1, l2, d, num_levels)
     ws = workspace(X.device, nb)
-    pm = L.PAIRS_UPPER if sym else L.PAIRS_RECT
     if state is not None:
         if order != 1 or not difference:
             raise ValueError("the saved VJP state needs order=1 and difference=True")

@@ -88,6 +88,11 @@ enum gpsig_out_mode {
  *     entry (b, a) is also stored when b lies in that row window.
  */
 size_t gpsig_sig_workspace_bytes(int n1, int l1, int n2, int l2, int d);
+/* The workspace of one gpsig_sig_gram / gpsig_sig_diag call given its order and pair mode: as above,
+ * except the higher-order recursion past 32 channels (linear base kernel only), whose cells come from
+ * an increment-Gram tile -- the reference's tf.matmul of the linear base kernel (kernels.py:1042-1044) --
+ * built by a matrix-core GEMM per chunk of x-rows: the increments plus one chunk's tile (<= 1 GiB). */
+size_t gpsig_sig_workspace_bytes_ex(int n1, int l1, int n2, int l2, int d, int order, int pair_mode);
 /* Extra workspace of a GPSIG_GRAM_SPLIT call (one chunk of pairs' cells); 0 where the split does not apply. */
 size_t gpsig_sig_split_bytes(int l1, int l2, int d, int num_levels);
 

@@ -270,3 +270,32 @@ def test_wide_rescaled(embedding):
         exp = sigalgs.signature_kern_rescaled_higher_order(np.einsum("npqd,rtd->nprtq", E, Zc), M)
     got = ops.rescaled(t(Z), t(X), M, embedding=embedding).cpu().numpy()
     assert (norm_rel_err(got[1:], exp[1:], axis_levels=True) < TOL).all()
+
+
+# ----------------------------------------------------------------------------- higher order, tile mode
+@pytest.mark.parametrize("D,L,M,order", [(46, 40, 4, 2), (63, 60, 5, 5), (40, 150, 5, 5), (100, 30, 4, 4)])
+def test_wide_higher_order_linear(D, L, M, order):
+    """Higher-order recursion past 32 channels with the linear base kernel (the exact signature kernel at
+    order >= M, as benchmarks/models/train_gpsig_vosf.py:102 trains it with add_time: 63 channels for
+    CMUsubject16): cells from the increment-Gram tile (a matrix-core GEMM), recursion as sig_ho; L = 150
+    runs in column blocks.  Cross, symmetric and diagonal against the fp64 oracle."""
+    from gpsig_amd import ops
+    rng = np.random.default_rng(D + L + order)
+    X, Y = walks(rng, 4, L, D), walks(rng, 3, L - 7, D)
+    ref = kr.SignatureKernelRef(L * D, D, M, normalization=False, base="linear", order=order)
+    got = ops.sig_gram(t(X), t(Y), M, order=order, base="linear").cpu().numpy()
+    assert (norm_rel_err(got[1:], ref.K_seq(X, Y)[1:], axis_levels=True) < TOL).all()
+    S = ops.sig_gram(t(X), None, M, order=order, base="linear").cpu().numpy()
+    exp = ref.K_seq(X, X)
+    assert (norm_rel_err(S[1:], exp[1:], axis_levels=True) < TOL).all()
+    d = ops.sig_diag(t(X), M, order=order, base="linear").cpu().numpy()
+    assert (norm_rel_err(d[1:], np.stack([np.diagonal(e) for e in exp])[1:], axis_levels=True) < TOL).all()
+
+
+def test_wide_higher_order_rbf_raises():
+    """The tile mode builds linear cells only: the RBF higher-order recursion past 32 channels raises."""
+    from gpsig_amd import _lib as Lb
+    from gpsig_amd import ops
+    X = torch.zeros((2, 10, 40), device=DEV)
+    with pytest.raises(Lb.GpsigError):
+        ops.sig_gram(X, None, 3, order=2, base="rbf")
