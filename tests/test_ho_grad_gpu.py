@@ -162,3 +162,19 @@ def test_higher_order_vjp_unsupported_raises():
     X = torch.zeros((2, 300, 2), device=DEV)
     with pytest.raises(Lb.GpsigError):
         ops.sig_gram_vjp(X, None, 3, torch.zeros((4, 2, 2), device=DEV), gout_levels=True, order=2)
+
+
+@pytest.mark.parametrize("L1,L2,D", [(2, 2, 3), (3, 40, 2), (2, 9, 40)])
+def test_higher_order_vjp_short_sequences(L1, L2, D):
+    """Order-2 VJP with one- and two-increment sequences (the recursion's shortest grids), cross pairs."""
+    from gpsig_amd import ops
+    M = 3
+    X, Y = _walks(2, L1, D, L1 + L2), _walks(3, L2, D, L1 + L2 + 1)
+    G = np.random.default_rng(5).standard_normal((M + 1, 2, 3))
+    gX, gY = ops.sig_gram_vjp(torch.tensor(X, device=DEV, dtype=torch.float32),
+                              torch.tensor(Y, device=DEV, dtype=torch.float32), M,
+                              torch.tensor(G, device=DEV), base="rbf", gout_levels=True, order=2)
+    Xr, Yr = torch.tensor(X, requires_grad=True), torch.tensor(Y, requires_grad=True)
+    (ar.k_seq(Xr, Yr, M, "rbf", order=2) * torch.tensor(G)).sum().backward()
+    assert norm_rel_err(gX.cpu().numpy(), Xr.grad.numpy()) < GTOL
+    assert norm_rel_err(gY.cpu().numpy(), Yr.grad.numpy()) < GTOL

@@ -299,3 +299,43 @@ def test_wide_higher_order_rbf_raises():
     X = torch.zeros((2, 10, 40), device=DEV)
     with pytest.raises(Lb.GpsigError):
         ops.sig_gram(X, None, 3, order=2, base="rbf")
+
+
+# ----------------------------------------------------------------------------- edge cases
+@pytest.mark.parametrize("D,L1,L2", [(33, 2, 2), (40, 2, 17), (64, 3, 130), (50, 129, 2)])
+def test_wide_edge_lengths(D, L1, L2):
+    """Shortest sequences (one increment), ragged lengths across the 128-point geometry switch, one
+    sequence per side: raw levels of the RBF and linear Gram against the oracle."""
+    from gpsig_amd import ops
+    rng = np.random.default_rng(D + L1 + L2)
+    X, Y = walks(rng, 1, L1, D), walks(rng, 2, L2, D)
+    for base in ("rbf", "linear"):
+        ref = kr.SignatureKernelRef(L1 * D, D, 4, normalization=False, base=base)
+        got = ops.sig_gram(t(X), t(Y), 4, base=base).cpu().numpy()
+        assert (norm_rel_err(got[1:], ref.K_seq(X, Y)[1:], axis_levels=True) < TOL).all(), base
+
+
+def test_wide_empty_and_single():
+    """An empty batch returns an empty Gram (the reference's graph does the same); N = 1 symmetric."""
+    from gpsig_amd import ops
+    X0 = torch.zeros((0, 20, 40), device=DEV)
+    assert ops.sig_gram(X0, None, 3).shape == (4, 0, 0)
+    rng = np.random.default_rng(1)
+    X = walks(rng, 1, 20, 40)
+    ref = kr.SignatureKernelRef(20 * 40, 40, 3, normalization=False)
+    got = ops.sig_gram(t(X), None, 3).cpu().numpy()
+    assert (norm_rel_err(got[1:], ref.K_seq(X, X)[1:], axis_levels=True) < TOL).all()
+
+
+@pytest.mark.parametrize("L", [2, 3, 65])
+def test_wide_higher_order_and_pde_short(L):
+    """Tile modes at the shortest lengths: higher-order linear (d = 40) and the PDE (d = 40, dyadic 2)."""
+    from gpsig_amd import ops
+    from oracle import pde
+    rng = np.random.default_rng(L)
+    X, Y = walks(rng, 3, L, 40), walks(rng, 2, L, 40)
+    ref = kr.SignatureKernelRef(L * 40, 40, 3, normalization=False, base="linear", order=3)
+    got = ops.sig_gram(t(X), t(Y), 3, order=3, base="linear").cpu().numpy()
+    assert (norm_rel_err(got[1:], ref.K_seq(X, Y)[1:], axis_levels=True) < TOL).all()
+    gp = ops.pde_gram(t(X), t(Y), 2, 1).cpu().numpy()
+    assert norm_rel_err(gp, pde.pde_gram(X, Y, 2, 1)) < TOL
