@@ -73,7 +73,7 @@ __global__ __launch_bounds__(256) void sig_bwd_wide_kernel(BwdArgs p) {
   const int nrows = DIFF ? l1 - 1 : l1;
 
   Seed seed;
-  seed.init(p.wd, p.lw2, fx, fy, gl, l2);
+  seed.init(p.wd, p.lw1, p.lw2, fx, fy, gl, l2);
   if constexpr (SEED == SEED_RBF_DIFF) seed.bound_c(nrows);
   bool colv[W], ptv[W];
 #pragma unroll

@@ -129,7 +129,7 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
     const int npts = nblk == 1 ? p.l2 : min(p.l2 - j0, DIFF ? CPB + 1 : CPB);
     PSeed seed;
     if constexpr (WIDE)
-      seed.init(p.wd, p.lw2, fx, fy + j0, gl, npts);
+      seed.init(p.wd, p.lw1, p.lw2, fx, fy + j0, gl, npts);
     else
       seed.init(fx, fy + (long long)j0 * FS, gl, npts);
 #ifndef GPSIG_CLO

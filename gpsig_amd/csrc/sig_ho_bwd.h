@@ -119,7 +119,7 @@ __global__ __launch_bounds__(256) void sig_ho_bwd_kernel(BwdArgs p) {
   const int nrows = l1 - 1;
 
   Seed seed;
-  seed.init(p.wd, p.lw2, fx, fy, lane, l2);
+  seed.init(p.wd, p.lw1, p.lw2, fx, fy, lane, l2);
   if constexpr (RBF) seed.bound_c(nrows);
   bool colv[W], ptv[W];
 #pragma unroll

@@ -55,7 +55,7 @@ struct RbfSeedWide {
   static constexpr int ANCHOR = GPSIG_PK_ANCHOR;
   static constexpr float NHL2E = -0.72134752044448170f;
   static constexpr float L2E = 1.4426950408889634f;
-  int d, lw;
+  int d, lw, lwx;  // channel count, record stride of the y (column) and x (row) sequences
   cfloat *fx;         // row side: the x-sequence's record (wave-uniform, scalar loads)
   const float *fyc;   // column side: the y-sequence's record at this lane's first column
   float mlast;        // 0 when the lane's column W-1 is a column block's halo point (no cell)
@@ -81,10 +81,11 @@ struct RbfSeedWide {
     }
   }
 
-  GPSIG_DEV void init(int d_, int lw_, const float *__restrict__ fxr, const float *__restrict__ fyblk, int gl,
+  GPSIG_DEV void init(int d_, int lwx_, int lw_, const float *__restrict__ fxr, const float *__restrict__ fyblk, int gl,
                       int npts) {
     d = d_;
     lw = lw_;
+    lwx = lwx_;
     fx = as_const(fxr);
     fyc = fyblk + gl * W;
     const int ncols = npts - 1;
@@ -99,7 +100,7 @@ struct RbfSeedWide {
 
   GPSIG_DEV void bound_c(int nrows) {
     float hx = 0.0f, hy = 0.0f;
-    cfloat *hr = fx + (long long)2 * d * lw;
+    cfloat *hr = fx + (long long)2 * d * lwx;
     for (int i = (int)__lane_id(); i < nrows; i += 64) hx = __builtin_fmaxf(hx, hr[i]);
 #pragma unroll
     for (int w2 = 0; w2 < W2; ++w2) hy = __builtin_fmaxf(hy, __builtin_fmaxf(hdy[w2][0], hdy[w2][1]));
@@ -108,7 +109,7 @@ struct RbfSeedWide {
     clo = wave_uniform(4.0f * hx * hy < 0.98f * EM1_LO_TAU * EM1_LO_TAU ? 1 : 0) != 0;
   }
 
-  // expm1(q) and k(x, y) of the row whose point is xr[k * lw] (channel k), from x - y
+  // expm1(q) and k(x, y) of the row whose point is xr[k * lwx] (channel k), from x - y
   GPSIG_DEV void exact(cfloat *xr, f2 (&Eqo)[W2], f2 (&ko)[W2]) const {
     f2 s[W2], qq[W2];
 #pragma unroll
@@ -119,7 +120,7 @@ struct RbfSeedWide {
     const float *yb = fyc, *dyb = fyc + (long long)d * lw;
 #pragma unroll 2
     for (int k = 0; k < d; ++k) {
-      const float xv = xr[(long long)k * lw];
+      const float xv = xr[(long long)k * lwx];
       float yv[W], dv[W];
       lcols(yb, k, yv);
       lcols(dyb, k, dv);
@@ -145,8 +146,8 @@ struct RbfSeedWide {
 
   // c_ij and the pair-0 p_ij of rows i0 .. i0+R-1 (rows past the sequence read its zero padding)
   GPSIG_DEV void chunk(int i0) {
-    cfloat *dxr = fx + (long long)d * lw + i0;
-    cfloat *gr = fx + (long long)(2 * d + 1) * lw + i0;
+    cfloat *dxr = fx + (long long)d * lwx + i0;
+    cfloat *gr = fx + (long long)(2 * d + 1) * lwx + i0;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
       pc[r] = splat2(-gr[r]);
@@ -157,7 +158,7 @@ struct RbfSeedWide {
     for (int k = 0; k < d; ++k) {
       float xr[R];
 #pragma unroll
-      for (int r = 0; r < R; ++r) xr[r] = dxr[(long long)k * lw + r];
+      for (int r = 0; r < R; ++r) xr[r] = dxr[(long long)k * lwx + r];
       float dv[W];
       lcols(dyb, k, dv);
       dv[W - 1] *= mlast;
@@ -266,7 +267,7 @@ struct WideSeedGen {
   static constexpr int ANCHOR = 1 << 30;
   static constexpr bool DIFF = SEED == SEED_LIN_DIFF;
   static constexpr float NHL2E = -0.72134752044448170f;
-  int d, lw;
+  int d, lw, lwx;  // channel count, record stride of the y (column) and x (row) sequences
   cfloat *fx;
   const float *fyc;
   f2 msk[W2];   // 1 for the lane's columns that are cells of the grid, 0 otherwise
@@ -288,10 +289,11 @@ struct WideSeedGen {
     }
   }
 
-  GPSIG_DEV void init(int d_, int lw_, const float *__restrict__ fxr, const float *__restrict__ fyblk, int gl,
+  GPSIG_DEV void init(int d_, int lwx_, int lw_, const float *__restrict__ fxr, const float *__restrict__ fyblk, int gl,
                       int npts) {
     d = d_;
     lw = lw_;
+    lwx = lwx_;
     fx = as_const(fxr);
     fyc = fyblk + gl * W;
     const int ncols = DIFF ? npts - 1 : npts;
@@ -304,7 +306,7 @@ struct WideSeedGen {
 
   GPSIG_DEV void chunk(int i0) {
     // rows: dx (LIN_DIFF) or x (POINT seeds); columns: dy or y
-    cfloat *xr0 = fx + (DIFF ? (long long)d * lw : 0) + i0;
+    cfloat *xr0 = fx + (DIFF ? (long long)d * lwx : 0) + i0;
     const float *yb = fyc + (DIFF ? (long long)d * lw : 0);
 #pragma unroll
     for (int r = 0; r < R; ++r)
@@ -313,7 +315,7 @@ struct WideSeedGen {
     for (int k = 0; k < d; ++k) {
       float xr[R];
 #pragma unroll
-      for (int r = 0; r < R; ++r) xr[r] = xr0[(long long)k * lw + r];
+      for (int r = 0; r < R; ++r) xr[r] = xr0[(long long)k * lwx + r];
       float yv[W];
       lcols(yb, k, yv);
 #pragma unroll

@@ -339,3 +339,31 @@ def test_wide_higher_order_and_pde_short(L):
     assert (norm_rel_err(got[1:], ref.K_seq(X, Y)[1:], axis_levels=True) < TOL).all()
     gp = ops.pde_gram(t(X), t(Y), 2, 1).cpu().numpy()
     assert norm_rel_err(gp, pde.pde_gram(X, Y, 2, 1)) < TOL
+
+
+@pytest.mark.parametrize("L1,L2", [(3, 130), (130, 9), (20, 300)])
+def test_wide_vjp_ragged_records(L1, L2):
+    """x and y records of different padded lengths (wide_lw(L1) != wide_lw(L2)): the row side strides by
+    the x record, the columns by the y record, in the forward seed and the VJP's regenerated cells."""
+    from gpsig_amd import ops
+    from oracle import autodiff_ref as ar
+    D, M = 46, 3
+    rng = np.random.default_rng(L1 * 7 + L2)
+    X, Y = walks(rng, 2, L1, D), walks(rng, 3, L2, D)
+    G = rng.standard_normal((M + 1, 2, 3))
+    Xt, Yt = t(X).float(), t(Y).float()
+    got = ops.sig_gram(Xt, Yt, M).cpu().numpy()
+    ref = kr.SignatureKernelRef(L1 * D, D, M, normalization=False)
+    assert (norm_rel_err(got[1:], ref.K_seq(X, Y)[1:], axis_levels=True) < TOL).all()
+    gX, gY = ops.sig_gram_vjp(Xt, Yt, M, torch.tensor(G, device=DEV, dtype=torch.float32), gout_levels=True)
+    Xr, Yr = torch.tensor(X, requires_grad=True), torch.tensor(Y, requires_grad=True)
+    (ar.k_seq(Xr, Yr, M, "rbf") * torch.tensor(G)).sum().backward()
+    assert norm_rel_err(gX.cpu().numpy(), Xr.grad.numpy()) < GTOL
+    assert norm_rel_err(gY.cpu().numpy(), Yr.grad.numpy()) < GTOL
+    if L2 <= 256:  # the higher-order VJP's range
+        gX2, gY2 = ops.sig_gram_vjp(Xt, Yt, M, torch.tensor(G, device=DEV, dtype=torch.float32), gout_levels=True,
+                                    order=2)
+        Xr, Yr = torch.tensor(X, requires_grad=True), torch.tensor(Y, requires_grad=True)
+        (ar.k_seq(Xr, Yr, M, "rbf", order=2) * torch.tensor(G)).sum().backward()
+        assert norm_rel_err(gX2.cpu().numpy(), Xr.grad.numpy()) < GTOL
+        assert norm_rel_err(gY2.cpu().numpy(), Yr.grad.numpy()) < GTOL
