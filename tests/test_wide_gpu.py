@@ -367,3 +367,29 @@ def test_wide_vjp_ragged_records(L1, L2):
         (ar.k_seq(Xr, Yr, M, "rbf", order=2) * torch.tensor(G)).sum().backward()
         assert norm_rel_err(gX2.cpu().numpy(), Xr.grad.numpy()) < GTOL
         assert norm_rel_err(gY2.cpu().numpy(), Yr.grad.numpy()) < GTOL
+
+
+@pytest.mark.parametrize("path", ["wide", "ho_tile", "pde_tile", "pde_sub"])
+def test_tile_paths_row_windows(path):
+    """Row windows (rows=(r0, r1), the row sharding of gpsig_amd/distributed.py) on the wide and tile
+    paths: every evaluated entry (a in the window, b >= a) equals the full symmetric call's."""
+    from gpsig_amd import ops
+    rng = np.random.default_rng(11)
+    n = 13
+    if path == "wide":
+        X = t(walks(rng, n, 40, 46)).float()
+        full = ops.sig_gram(X, None, 3)
+        part = lambda r0, r1: ops.sig_gram(X, None, 3, rows=(r0, r1))  # noqa: E731
+    elif path == "ho_tile":
+        X = t(walks(rng, n, 30, 40)).float()
+        full = ops.sig_gram(X, None, 4, order=2, base="linear")
+        part = lambda r0, r1: ops.sig_gram(X, None, 4, order=2, base="linear", rows=(r0, r1))  # noqa: E731
+    else:
+        dy = 1 if path == "pde_tile" else 5
+        X = t(walks(rng, n, 20, 40 if path == "pde_tile" else 3)).float()
+        full = ops.pde_gram(X, None, dy, 1)[None]
+        part = lambda r0, r1: ops.pde_gram(X, None, dy, 1, rows=(r0, r1))[None]  # noqa: E731
+    for r0, r1 in [(0, 5), (5, 6), (6, 13), (3, 11)]:
+        got = part(r0, r1)
+        for a in range(r0, r1):
+            torch.testing.assert_close(got[:, a - r0, a:], full[:, a, a:], rtol=1e-6, atol=1e-7)
