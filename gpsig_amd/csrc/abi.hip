@@ -8,7 +8,7 @@
 namespace gpsig {
 int features(const float *X, int n, int l, int d, int DP, float *F, hipStream_t s);
 int sig_fo_launch(const SigArgs &a, int DP, int seed, long long nblocks, hipStream_t s);
-int fo_lanes_per_pair(int l2, int DP, int M, bool mf, int seed);
+int fo_lanes_per_pair(int l2, int DP, int M, bool mf, int seed, bool split);
 size_t fo_split_bytes(int l1, int l2, int DP, int M);
 int sig_ho_launch(const SigArgs &a, int DP, int seed, long long nblocks, hipStream_t s);
 bool ho_tiled(int d, int order);
@@ -90,7 +90,6 @@ extern "C" size_t gpsig_sig_split_bytes(int l1, int l2, int d, int num_levels) {
   return fo_split_bytes(l1, l2, DP, num_levels);
 }
 
-static inline long long upper_prefix(long long r, long long ntb, long long k) { return r * ntb - k * r * (r - 1) / 2; }
 
 static int sig_gram_impl(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int num_levels,
                          int order, int base_kind, int difference, int pair_mode, int row_begin, int row_end,
@@ -179,7 +178,7 @@ static int sig_gram_impl(const float *X, int n1, int l1, const float *Y, int n2,
   a.sx = wide_rec_floats(d, l1);
   a.sy = wide_rec_floats(d, l2);
 
-  const int LP = (order == 1) ? fo_lanes_per_pair(l2, DP, num_levels, mfma, seed) : ho_lanes_per_pair(l2, order, num_levels);
+  const int LP = (order == 1) ? fo_lanes_per_pair(l2, DP, num_levels, mfma, seed, split) : ho_lanes_per_pair(l2, order, num_levels);
   if (LP == 0) return GPSIG_EUNSUPPORTED;
   const int G = 64 / LP;
   long long nblocks = 0;
@@ -194,9 +193,9 @@ static int sig_gram_impl(const float *X, int n1, int l1, const float *Y, int n2,
     if (pair_mode == GPSIG_PAIRS_RECT) {
       nblocks = (long long)(ta1 - ta0) * ntb;
     } else {
-      const int k = 4 / G;
-      a.tile_base = upper_prefix(ta0, ntb, k);
-      nblocks = upper_prefix(ta1, ntb, k) - a.tile_base;
+      // tile row r starts at B tile floor(4 r / G) (G = 6 for the 10-lane groups: not a whole ratio)
+      a.tile_base = upper_prefix_g(ta0, ntb, G);
+      nblocks = upper_prefix_g(ta1, ntb, G) - a.tile_base;
     }
   }
   if (nblocks > 0x7fffffffLL) return GPSIG_EUNSUPPORTED;

@@ -71,6 +71,50 @@ GPSIG_DEV void group_incl_scan_n(float (&v)[N]) {
   }
 }
 
+// Lane groups that are not aligned to DPP rows: LP = 10 or 20 lanes per group, groups at lanes 0, LP,
+// 2 LP, ... (64 / LP of them; the remaining lanes form a partial group whose results are discarded).
+// Every such group spans at most two 16-lane rows (group starts fall at row offsets 0, 10, 4, 14, 8, 2
+// for LP = 10 and 0, 4, 8 for LP = 20), so a segmented Hillis-Steele scan needs the four in-row steps
+// (row_shr, whose out-of-row sources read 0) with the term weighted by a per-lane 0/1 factor (source in
+// the same group: gl >= s), plus one row_bcast:15 step taken by the lanes whose group began in the
+// previous row (lane 15 of that row then holds the group's sum from its start).  Five DPP steps, as
+// the LP = 32 scan.
+template <int LP>
+struct SegFactors {
+  float f1, f2, f4, f8, fb;
+  GPSIG_DEV SegFactors() {
+    const int lane = (int)__lane_id(), gl = lane % LP, rl = lane & 15;
+    f1 = gl >= 1 ? 1.0f : 0.0f;
+    f2 = gl >= 2 ? 1.0f : 0.0f;
+    f4 = gl >= 4 ? 1.0f : 0.0f;
+    f8 = gl >= 8 ? 1.0f : 0.0f;
+    fb = gl > rl ? 1.0f : 0.0f;
+  }
+};
+template <int LP, int N>
+GPSIG_DEV void seg_incl_scan_n(float (&v)[N], const SegFactors<LP> &f) {
+  static_assert(LP == 10 || LP == 20, "segmented groups");
+#pragma unroll
+  for (int k = 0; k < N; ++k) v[k] = __builtin_fmaf(dpp_f<0x111>(v[k]), f.f1, v[k]);
+#pragma unroll
+  for (int k = 0; k < N; ++k) v[k] = __builtin_fmaf(dpp_f<0x112>(v[k]), f.f2, v[k]);
+#pragma unroll
+  for (int k = 0; k < N; ++k) v[k] = __builtin_fmaf(dpp_f<0x114>(v[k]), f.f4, v[k]);
+#pragma unroll
+  for (int k = 0; k < N; ++k) v[k] = __builtin_fmaf(dpp_f<0x118>(v[k]), f.f8, v[k]);
+#pragma unroll
+  for (int k = 0; k < N; ++k) v[k] = __builtin_fmaf(dpp_f<0x142>(v[k]), f.fb, v[k]);
+}
+// Sum over a segmented group (LP = 10 / 20), valid in the group's first lane (gl == 0).
+template <int LP>
+GPSIG_DEV float seg_group_sum(float v, const SegFactors<LP> &f) {
+  float t[1] = {v};
+  seg_incl_scan_n<LP, 1>(t, f);
+  const int lane = (int)__lane_id();
+  const int last = lane - lane % LP + LP - 1;
+  return __shfl(t[0], last < 64 ? last : 63, 64);
+}
+
 // Value of lane (lane+1) of the wave (0 for lane 63).
 GPSIG_DEV float lane_next(float v) { return dpp_f<0x130>(v); }
 // Value of lane (lane-1) of the wave (`edge` for lane 0 is handled by the caller).

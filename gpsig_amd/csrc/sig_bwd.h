@@ -90,7 +90,10 @@ GPSIG_DEV void group_excl_cols_n(const float (&v)[N][W], float (&out)[N][W]) {
     t[n] = s;
     incl[n] = s;
   }
-  group_incl_scan_n<LP, N>(incl);
+  if constexpr (64 % LP != 0)
+    seg_incl_scan_n<LP, N>(incl, SegFactors<LP>{});
+  else
+    group_incl_scan_n<LP, N>(incl);
 #pragma unroll
   for (int n = 0; n < N; ++n) {
     float run = incl[n] - t[n];
@@ -114,8 +117,15 @@ GPSIG_DEV void group_rexcl_cols_n(const float (&v)[N][W], float (&out)[N][W]) {
     t[n] = s;
     incl[n] = s;
   }
-  group_incl_scan_n<LP, N>(incl);
-  const int last = (int)(__lane_id() | (LP - 1));
+  int last;
+  if constexpr (64 % LP != 0) {  // segmented groups (LP = 20): the group's last lane, the idle tail clamped
+    seg_incl_scan_n<LP, N>(incl, SegFactors<LP>{});
+    const int l0 = (int)__lane_id() - (int)__lane_id() % LP + LP - 1;
+    last = l0 < 64 ? l0 : 63;
+  } else {
+    group_incl_scan_n<LP, N>(incl);
+    last = (int)(__lane_id() | (LP - 1));
+  }
 #pragma unroll
   for (int n = 0; n < N; ++n) {
     const float tot = __shfl(incl[n], last, 64);
@@ -197,6 +207,7 @@ template <int DP, int W, int LP, int M, int SEED>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_WPE))) void sig_bwd_kernel(BwdArgs p) {
   constexpr int FS = feat_stride(DP);
   constexpr int G = 64 / LP;
+  constexpr bool SEG = (64 % LP) != 0;  // LP = 20: 3 pairs per wave, lanes 60..63 idle (common.h)
   constexpr bool DIFF = (SEED == SEED_RBF_DIFF || SEED == SEED_LIN_DIFF);  // else difference=False
   constexpr bool RBF = (SEED == SEED_RBF_DIFF || SEED == SEED_RBF_POINT);   // base kernel
   constexpr float NHL2E = -0.72134752044448170f;  // exp(-d2/2) = exp2(d2 * NHL2E)
@@ -227,7 +238,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
   } else {
     int ta, tb;
     if (p.pair_mode == GPSIG_PAIRS_UPPER) {
-      const Tile t = upper_tile(p.tile_base + lblk, p.ntb, 4 / G);
+      Tile t;
+      if constexpr (SEG)
+        t = upper_tile_g<G>(p.tile_base + lblk, p.ntb);
+      else
+        t = upper_tile(p.tile_base + lblk, p.ntb, 4 / G);
       ta = t.ta;
       tb = t.tb;
     } else {
@@ -235,11 +250,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
       tb = (int)(lblk % p.ntb);
     }
     a = ta * 4 + wave;
-    b = tb * G + g;
+    b = tb * G + (SEG && g >= G ? G - 1 : g);  // the idle lanes shadow the last group's pair
     if (a < p.row_begin || a >= p.row_end) return;  // wave-uniform
   }
   bool pair_ok = b < p.n2;
   if (p.pair_mode == GPSIG_PAIRS_UPPER) pair_ok = pair_ok && b >= a;
+  if (SEG) pair_ok = pair_ok && g < G;
   if (diag) pair_ok = (g == 0);
   const int bl = b < p.n2 ? b : p.n2 - 1;
   const int l1 = p.l1, l2 = p.l2;
@@ -426,7 +442,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
         float s = 0.0f;
 #pragma unroll
         for (int w = 0; w < W; ++w) s += C[m][w];
-        Kacc[m] += group_sum<LP>(s);
+        if constexpr (SEG)
+          Kacc[m] += seg_group_sum<LP>(s, SegFactors<LP>{});
+        else
+          Kacc[m] += group_sum<LP>(s);
       }
       if (blocked) {  // this block's end state, for its reverse sweep
 #pragma unroll
@@ -873,7 +892,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
 // y, dy and the y-gradient accumulator (3 W DP floats) plus 2 (M-1) W level states.  Longer sequences
 // run at LP = 64 in column blocks of 64 W - 1 cells (BwdArgs::nblk).
 struct BwdGeo { int W, LP; };
-inline BwdGeo bwd_geometry(int l2, int DP) {
+// 20-lane groups of 5 columns (3 pairs per wave, segmented scans, common.h) for 65..100 points: 100
+// columns per pair instead of LP = 32 x W = 4 = 128, and 5 DPP steps per scan instead of 6 (N = 1024,
+// L = 100, D = 5, M = 5, tools/kbench_vjp.hip: 29.9 -> 23.6 ms).  Within 256 VGPRs at 2 waves/SIMD for
+// DP <= 5, M <= 6.
+constexpr bool bwd_seg_ok(int DP, int M) { return DP >= 1 && DP <= 5 && M <= 6; }
+inline BwdGeo bwd_geometry(int l2, int DP, int M = 0) {
+#ifndef GPSIG_BWD_SEG
+#define GPSIG_BWD_SEG 1
+#endif
+  if (GPSIG_BWD_SEG && M > 0 && bwd_seg_ok(DP, M) && l2 > 64 && l2 <= 100) return {5, 20};
   const int W = DP <= 8 ? 4 : 2;
   for (int LP : {16, 32, 64})
     if (LP * W >= l2) return {W, LP};

@@ -58,7 +58,6 @@ __global__ void gscale_reduce_kernel(const float *__restrict__ slots, int levels
   for (int k = 0; k < GSCALE_SLOTS; ++k) s += slots[k * levels + m];
   gscale[m] += s;
 }
-static inline long long upper_prefix(long long r, long long ntb, long long k) { return r * ntb - k * r * (r - 1) / 2; }
 
 // The VJPs with point-weight tiles and emission GEMMs (sig_bwd_wide.hip): order 1 at wide channel counts,
 // and every order > 1
@@ -130,7 +129,7 @@ extern "C" int gpsig_sig_gram_vjp(const float *X, int n1, int l1, const float *Y
   if (wide)
     return tile_vjp(X, n1, l1, Y, n2, l2, d, num_levels, 1, seed, pair_mode, row_begin, row_end, gout, gout_levels,
                     rs1, rs2, scale, jitter, gX, gY, grs1, grs2, gscale, state, workspace, workspace_bytes, s);
-  const BwdGeo geo = bwd_geometry(l2, DP);
+  const BwdGeo geo = bwd_geometry(l2, DP, num_levels);
   if (geo.W == 0) return GPSIG_EUNSUPPORTED;
   if (row_end == row_begin) return GPSIG_OK;
   const int nblk = bwd_blocks(l2, difference != 0, geo);
@@ -188,9 +187,8 @@ extern "C" int gpsig_sig_gram_vjp(const float *X, int n1, int l1, const float *Y
     if (pair_mode == GPSIG_PAIRS_RECT) {
       nblocks = (long long)(ta1 - ta0) * ntb;
     } else {
-      const int k = 4 / G;
-      a.tile_base = upper_prefix(ta0, ntb, k);
-      nblocks = upper_prefix(ta1, ntb, k) - a.tile_base;
+      a.tile_base = upper_prefix_g(ta0, ntb, G);
+      nblocks = upper_prefix_g(ta1, ntb, G) - a.tile_base;
     }
   }
   if (nblocks > 0x7fffffffLL) return GPSIG_EUNSUPPORTED;

@@ -12,7 +12,9 @@ static int launch_bwd(const BwdArgs &a, long long nblocks, hipStream_t s) {
 
 template <int DP, int M, int SEED>
 static int bwd_geo(const BwdArgs &a, long long nblocks, hipStream_t s) {
-  const BwdGeo geo = bwd_geometry(a.l2, DP);
+  const BwdGeo geo = bwd_geometry(a.l2, DP, M);
+  if constexpr (bwd_seg_ok(DP, M))
+    if (geo.W == 5 && geo.LP == 20) return launch_bwd<DP, 5, 20, M, SEED>(a, nblocks, s);
   constexpr int W = DP <= 8 ? 4 : 2;
   if (geo.W != W) return GPSIG_EUNSUPPORTED;
   switch (geo.LP) {

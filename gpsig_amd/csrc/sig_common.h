@@ -259,7 +259,8 @@ struct RbfSeedPk {
 #ifndef GPSIG_YG_DP
 #define GPSIG_YG_DP 6
 #endif
-  static constexpr bool YG = DP >= GPSIG_YG_DP;
+  // (W = 10, the 10-lane groups: also at any DP, to stay within 256 VGPRs)
+  static constexpr bool YG = DP >= GPSIG_YG_DP || W > 8;
   static constexpr int YR = YG ? 1 : W2;
   f2 y[YR][DP], dy[W2][DP], hdy[W2];
   f2 Eq[W2], kc[W2];  // expm1(q_ij), k(x_i, y_j)
@@ -280,7 +281,6 @@ struct RbfSeedPk {
     }
     return v;
   }
-
   GPSIG_DEV void init(const float *__restrict__ fx, const float *__restrict__ fy, int gl, int l2) {
     const int ncols = l2 - 1;
     fyb = fy;
@@ -583,6 +583,66 @@ GPSIG_DEV float level1_closed(const float *__restrict__ fx, const float *__restr
 // lane groups take b = G*tb + g.  UPPER enumerates only tiles with some b >= a: with k = 4/G,
 // tile row ta has ntb - k*ta tiles, prefix P(r) = r*ntb - k*r*(r-1)/2, inverted in closed form.
 struct Tile { int ta, tb; };
+
+// sum_{i < n} floor((a i + b) / m), n, m > 0, a, b >= 0 (Euclid-like reduction, O(log m) steps)
+__host__ __device__ inline long long floor_sum(long long n, long long m, long long a, long long b) {
+  long long ans = 0;
+  while (true) {
+    if (a >= m) {
+      ans += (n - 1) * n / 2 * (a / m);
+      a %= m;
+    }
+    if (b >= m) {
+      ans += n * (b / m);
+      b %= m;
+    }
+    const long long y = a * n + b;
+    if (y < m) break;
+    n = y / m;
+    b = y % m;
+    const long long t = m;
+    m = a;
+    a = t;
+  }
+  return ans;
+}
+// Tiles of the upper triangle when a tile row (4 sequences a) is not a whole number of B tiles (G = 6
+// sequences b per wave, LP = 10): tile row r begins at B tile floor(4 r / G) (the first holding some
+// b >= 4 r), so P(r) = r ntb - sum_{t < r} floor(4 t / G).
+__host__ __device__ inline long long upper_prefix_g(long long r, long long ntb, int G) {
+  return r * ntb - floor_sum(r, G, 4, 0);
+}
+// The same prefix with G a compile-time constant (the kernel's tile decoder: no runtime division).
+// With p / q = 4 / G in lowest terms and r = q Q + R, floor(p (q u + v) / q) = p u + floor(p v / q), so
+// sum_{t<r} floor(4t/G) = p q Q (Q-1)/2 + Q S + p Q R + sum_{v<R} floor(p v / q), S = sum_{v<q} floor(p v / q).
+template <int G>
+__host__ __device__ inline long long upper_prefix_c(long long r, long long ntb) {
+  constexpr int gg = G % 4 == 0 ? 4 : (G % 2 == 0 ? 2 : 1);
+  constexpr long long p = 4 / gg, q = G / gg;
+  long long S = 0;
+  for (long long v = 0; v < q; ++v) S += p * v / q;
+  const long long Q = r / q, R = r % q;
+  long long part = 0;
+  for (long long v = 0; v < R; ++v) part += p * v / q;
+  return r * ntb - (p * q * Q * (Q - 1) / 2 + Q * S + p * Q * R + part);
+}
+template <int G>
+GPSIG_DEV Tile upper_tile_g(long long t, int ntb) {
+  // continuous estimate: sum_{t<r} floor(4t/G) ~ (2/G) r (r - 1) - r (q - 1) / (2q), q = G / gcd(4, G)
+  // (the fractional parts average (q-1)/(2q)), so the exact prefixes correct it by a step or two
+  constexpr int q = G / (G % 4 == 0 ? 4 : (G % 2 == 0 ? 2 : 1));
+  const double A = 2.0 / G, B = ntb + 2.0 / G + (q - 1) / (2.0 * q);
+  double disc = B * B - 4.0 * A * (double)t;
+  disc = disc < 0 ? 0 : disc;
+  long long r = (long long)((B - __builtin_sqrt(disc)) / (2.0 * A));
+  if (r < 0) r = 0;
+  while (r > 0 && upper_prefix_c<G>(r, ntb) > t) --r;
+  while (upper_prefix_c<G>(r + 1, ntb) <= t) ++r;
+  Tile tl;
+  tl.ta = (int)r;
+  tl.tb = (int)(4 * r / G + (t - upper_prefix_c<G>(r, ntb)));
+  return tl;
+}
 
 GPSIG_DEV Tile upper_tile(long long t, int ntb, int k) {
   // largest r with P(r) <= t

@@ -46,7 +46,7 @@ struct FoRec<true, PK, PS, DP, W> { using type = typename PS::Row; };
 template <class PS, int DP, int W>
 struct FoRec<false, true, PS, DP, W> { using type = typename RbfSeedPk<DP, W>::Row; };
 
-__host__ __device__ constexpr int fo_waves(int DP, int W, int M) { return (W == 8 && DP > 6 && M <= 6) ? 2 : 1; }
+__host__ __device__ constexpr int fo_waves(int DP, int W, int M) { return ((W == 8 && DP > 6 && M <= 6) || W == 10) ? 2 : 1; }
 
 template <int DP, int W, int LP, int M, int SEED, bool DIAGK, bool SAVE = false, bool MF = false, int SPLIT = 0>
 #ifdef GPSIG_FO_LB
@@ -60,6 +60,8 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
   constexpr bool DIFF = SEED == SEED_RBF_DIFF || SEED == SEED_LIN_DIFF;
   constexpr int FS = feat_stride(DP);
   constexpr int G = 64 / LP;
+  // SEG: lane groups not aligned to DPP rows (LP = 10: G = 6 pairs per wave, lanes 60..63 idle)
+  constexpr bool SEG = (64 % LP) != 0;
 
   const int lane = threadIdx.x & 63;
   const int wave = wave_uniform(threadIdx.x >> 6);
@@ -76,7 +78,11 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
     int ta, tb;
     const long long lblk = p.blk0 + (long long)blockIdx.x;
     if (p.pair_mode == GPSIG_PAIRS_UPPER) {
-      const Tile t = upper_tile(p.tile_base + lblk, p.ntb, 4 / G);
+      Tile t;
+      if constexpr (SEG)
+        t = upper_tile_g<G>(p.tile_base + lblk, p.ntb);
+      else
+        t = upper_tile(p.tile_base + lblk, p.ntb, 4 / G);
       ta = t.ta;
       tb = t.tb;
     } else {
@@ -84,7 +90,7 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
       tb = (int)(lblk % p.ntb);
     }
     a = ta * 4 + wave;
-    b = tb * G + g;
+    b = tb * G + (SEG && g >= G ? G - 1 : g);  // the idle lanes shadow the last group's pair
     if (a < p.row_begin || a >= p.row_end) return;  // wave-uniform
   }
   static_assert(SPLIT == 0 || (!DIAGK && !SAVE && !MF && SEED == SEED_RBF_DIFF), "split: RBF Gram pairs only");
@@ -95,6 +101,7 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
     dms = p.dmbuf + (((long long)blockIdx.x * 4 + wave) * G + g) * (long long)(p.l1 - 1) * (LP * W) + (long long)gl * W;
   bool pair_ok = b < p.n2;
   if (p.pair_mode == GPSIG_PAIRS_UPPER) pair_ok = pair_ok && b >= a;
+  if (SEG) pair_ok = pair_ok && g < G;
   if (DIAGK) pair_ok = (g == 0);
   const int bl = b < p.n2 ? b : p.n2 - 1;
 
@@ -122,6 +129,8 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
   float Kacc[M];
 #pragma unroll
   for (int m = 0; m < M; ++m) Kacc[m] = 0.0f;
+  using SegF = std::conditional_t<SEG, SegFactors<SEG ? LP : 10>, char>;
+  const SegF segf{};
 
   for (int blk = 0; blk < nblk; ++blk) {
     const int j0 = blk * CPB;
@@ -198,7 +207,12 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
         T[m] = E[m][W2][0] + E[m][W2][1];
         base[m] = T[m];
       }
-      if constexpr (M > 1) group_incl_scan_n<LP, ML>(base);
+      if constexpr (M > 1) {
+        if constexpr (SEG)
+          seg_incl_scan_n<LP, ML>(base, segf);
+        else
+          group_incl_scan_n<LP, ML>(base);
+      }
       if constexpr (LP == 64 && M > 1) {
         if (nblk > 1) {  // wave-uniform: carry in from the blocks to the left, carry out to the right
           float *__restrict__ cr = carry + (long long)i * ML;
@@ -335,7 +349,10 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
       f2 s2 = C[m][0];
 #pragma unroll
       for (int w2 = 1; w2 < W2; ++w2) s2 += C[m][w2];
-      Kacc[m] += group_sum<LP>(s2[0] + s2[1]);
+      if constexpr (SEG)
+        Kacc[m] += seg_group_sum<LP>(s2[0] + s2[1], segf);
+      else
+        Kacc[m] += group_sum<LP>(s2[0] + s2[1]);
     }
   }
 
@@ -383,12 +400,20 @@ inline Geo fo_geometry_wide(int l2, int seed) {
     if (LP * 8 >= l2) return {8, LP};
   return {8, 64};
 }
-inline Geo fo_geometry(int l2, int DP, int M, bool mf = false) {
+// 10-lane groups of 10 columns (6 pairs per wave, SEG scans): sequences of 65..100 points take 100 of
+// a group's columns instead of LP = 16 x W = 8 = 128 (C2, L = 100: 99 cells per row on 100 columns
+// instead of 128).  RBF difference seed only, where W = 10 fits 256 VGPRs (DP <= 5, M <= 5).
+constexpr bool fo_seg_ok(int DP, int M, int seed) { return seed == SEED_RBF_DIFF && DP >= 1 && DP <= 5 && M <= 5; }
+inline Geo fo_geometry(int l2, int DP, int M, bool mf = false, int seed = -1) {
   if (mf) {  // matrix-core seed (RBF difference seed only): W = 4 columns per lane, no column blocks
     for (int LP : {16, 32, 64})
       if (LP * 4 >= l2) return {4, LP};
     return {0, 0};
   }
+#ifndef GPSIG_FO_SEG
+#define GPSIG_FO_SEG 1
+#endif
+  if (GPSIG_FO_SEG && fo_seg_ok(DP, M, seed) && l2 > 64 && l2 <= 100) return {10, 10};
   // smallest LP (shortest scans) at which some W <= fo_wmax covers the sequence, smallest such W
   for (int LP : {16, 32, 64})
     for (int W = 2; W <= fo_wmax(DP, M); W *= 2)
@@ -465,7 +490,7 @@ int fo_geo(const SigArgs &a, long long nblocks, hipStream_t s) {
   if constexpr (DP == 0) {  // wide channel counts
     return fo_geo_wide<M, SEED>(a, nblocks, s);
   } else {
-  const Geo geo = fo_geometry(a.l2, DP, M, a.mfma != 0);
+  const Geo geo = fo_geometry(a.l2, DP, M, a.mfma != 0, a.dmbuf ? -1 : SEED);  // split diagnostic: aligned groups
   if constexpr (SEED == SEED_RBF_DIFF) {
     if (a.mfma) {  // A/B variant: seed dots on the matrix cores (not for the saved-state launch)
       if (a.state) return GPSIG_EUNSUPPORTED;
@@ -492,6 +517,7 @@ int fo_geo(const SigArgs &a, long long nblocks, hipStream_t s) {
   GPSIG_GEO(2, 16) GPSIG_GEO(2, 32) GPSIG_GEO(2, 64)
   if constexpr (WM >= 4) { GPSIG_GEO(4, 16) GPSIG_GEO(4, 32) GPSIG_GEO(4, 64) }
   if constexpr (WM >= 8) { GPSIG_GEO(8, 16) GPSIG_GEO(8, 32) GPSIG_GEO(8, 64) }
+  if constexpr (fo_seg_ok(DP, M, SEED)) { GPSIG_GEO(10, 10) }
 #undef GPSIG_GEO
   return GPSIG_EUNSUPPORTED;
   }

@@ -79,7 +79,7 @@ static int fo_dp(const SigArgs &a, int seed, long long nblocks, hipStream_t s) {
 }
 
 int sig_fo_launch(const SigArgs &a0, int DP, int seed, long long nblocks, hipStream_t s) {
-  const Geo g = DP == 0 ? fo_geometry_wide(a0.l2, seed) : fo_geometry(a0.l2, DP, a0.M, a0.mfma != 0);
+  const Geo g = DP == 0 ? fo_geometry_wide(a0.l2, seed) : fo_geometry(a0.l2, DP, a0.M, a0.mfma != 0, a0.dmbuf ? -1 : seed);
   if (g.W == 0) return GPSIG_EUNSUPPORTED;
   SigArgs a = a0;
   a.nblk = fo_blocks(a0.l2, seed == SEED_RBF_DIFF || seed == SEED_LIN_DIFF, g);
@@ -92,8 +92,8 @@ int sig_fo_launch(const SigArgs &a0, int DP, int seed, long long nblocks, hipStr
   }
 }
 
-int fo_lanes_per_pair(int l2, int DP, int M, bool mf, int seed) {
-  return (DP == 0 ? fo_geometry_wide(l2, seed) : fo_geometry(l2, DP, M, mf)).LP;
+int fo_lanes_per_pair(int l2, int DP, int M, bool mf, int seed, bool split) {
+  return (DP == 0 ? fo_geometry_wide(l2, seed) : fo_geometry(l2, DP, M, mf, split ? -1 : seed)).LP;
 }
 
 // ------------------------------------------------------------------------------------ wide records

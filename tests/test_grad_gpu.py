@@ -98,6 +98,28 @@ def test_gram_vjp_shapes(D, M, L):
     assert norm_rel_err(got[0], ref[0]) < GTOL
 
 
+@pytest.mark.parametrize("base", ["rbf", "linear"])
+@pytest.mark.parametrize("N,D,M,L", [(13, 5, 5, 100), (7, 3, 6, 81), (10, 2, 4, 65), (5, 5, 5, 99)])
+def test_gram_vjp_twenty_lane_groups(base, N, D, M, L):
+    """65..100 points: the VJP runs 20-lane groups of 5 columns (3 pairs per wave, segmented scans) and
+    the forward 10-lane groups of 10 columns; K(X) and K(X, X2) gradients vs fp64 autodiff."""
+    import gpsig_amd
+    X = walks(N, L, D, 40 + N)
+    X2 = walks(N - 2, L, D, 41 + N)
+    cls = gpsig_amd.SignatureRBF if base == "rbf" else gpsig_amd.SignatureLinear
+    k = cls(L * D, D, M)
+    G = np.random.default_rng(N).standard_normal((N, N))
+    got, K = grads_gpu(k, X, None, G)
+    ref, _, _, Kref = grads_ref(X, None, G, M, base=base)
+    assert norm_rel_err(K, Kref) < 1e-5
+    assert norm_rel_err(got[0], ref[0]) < GTOL
+    G2 = np.random.default_rng(N + 1).standard_normal((N, N - 2))
+    got, _ = grads_gpu(k, X, X2, G2)
+    ref, _, _, _ = grads_ref(X, X2, G2, M, base=base)
+    for g, r in zip(got, ref):
+        assert norm_rel_err(g, r) < GTOL
+
+
 def test_kdiag_unnormalised_vjp():
     import gpsig_amd
     N, L, D, M = 7, 30, 3, 4

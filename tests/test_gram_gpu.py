@@ -107,9 +107,10 @@ def test_no_difference(base):
     assert (norm_rel_err(got[1:], g[f"{base}_nodiff"][1:], axis_levels=True) < TOL).all()
 
 
-@pytest.mark.parametrize("L", [2, 3, 17, 33, 64, 65, 128, 129, 200, 257, 300])
+@pytest.mark.parametrize("L", [2, 3, 17, 33, 64, 65, 81, 100, 101, 128, 129, 200, 257, 300])
 def test_lengths_and_geometries(L):
-    """Every lane-geometry branch (LP=16/32/64, W=4/8) incl. ragged edges, vs the oracle."""
+    """Every lane-geometry branch (LP=16/32/64, W=4/8, and the 10-lane groups of 10 columns at 65..100
+    points) incl. ragged edges, vs the oracle."""
     from gpsig_amd import ops
     rng = np.random.default_rng(L)
     N1, N2, D, M = 5, 3, 4, 4
@@ -133,6 +134,28 @@ def test_channels_and_levels(D, M):
     exp = kr.SignatureKernelRef(24 * D, D, M, normalization=False).K_seq(X)
     got = ops.sig_gram(t(X), None, M).cpu().numpy()
     assert (norm_rel_err(got[1:], exp[1:], axis_levels=True) < TOL).all()
+
+
+@pytest.mark.parametrize("N", [1, 5, 6, 7, 23, 61])
+def test_ten_lane_groups_tiles(N):
+    """The 10-lane geometry (6 pairs per wave, tile rows starting at B tile floor(4r/6)): every pair of
+    the upper triangle is evaluated exactly once and mirrored, for N around the tile sizes; D = 5, M = 5,
+    L = 100 (C2's shape), raw levels and the normalised sum, against the oracle."""
+    from gpsig_amd import ops
+    rng = np.random.default_rng(7 * N)
+    L, D, M = 100, 5, 5
+    X = np.cumsum(rng.standard_normal((N, L, D)), 1) / np.sqrt(L * D)
+    ref = kr.SignatureKernelRef(L * D, D, M, normalization=False)
+    got = ops.sig_gram(t(X), None, M).cpu().numpy()
+    assert (norm_rel_err(got[1:], ref.K_seq(X)[1:], axis_levels=True) < TOL).all()
+    # row windows of the upper-triangle launch (the distributed row shards): tile_base from the exact prefix
+    if N >= 7:
+        full = torch.as_tensor(got, device=DEV)
+        for r0, r1 in [(0, 3), (3, N // 2), (N // 2, N)]:
+            up = torch.zeros(M + 1, r1 - r0, N, device=DEV)
+            ops.sig_gram(t(X), None, M, rows=(r0, r1), out=up)
+            mask = torch.arange(N, device=DEV)[None, :] >= torch.arange(r0, r1, device=DEV)[:, None]
+            torch.testing.assert_close(up[:, mask], full[:, r0:r1][:, mask], rtol=1e-5, atol=1e-6)
 
 
 def test_row_windows_and_rect_tiles():

@@ -96,11 +96,11 @@ int main(int argc, char **argv) {
   p.out_ld = n;
   p.out_lvl = (long long)n * n;
   const Geo geo{KW, KLP};
-  const int G = 64 / geo.LP, k = 4 / G;
+  const int G = 64 / geo.LP;
   const long long ntb = (n + G - 1) / G, nta = (n + 3) / 4;
   p.ntb = (int)ntb;
   p.tile_base = 0;
-  const long long nblocks = nta * ntb - k * nta * (nta - 1) / 2;
+  const long long nblocks = upper_prefix_g(nta, ntb, G);
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));

@@ -94,10 +94,10 @@ int main(int argc, char **argv) {
   p.g_lvl = (long long)n * n;
   p.gX = p.gY = dGX;
   p.nblk = 1;
-  const int G_ = 64 / KLP, k = 4 / G_;
+  const int G_ = 64 / KLP;
   const long long ntb = (n + G_ - 1) / G_, nta = (n + 3) / 4;
   p.ntb = (int)ntb;
-  const long long nblocks = nta * ntb - k * nta * (nta - 1) / 2;
+  const long long nblocks = upper_prefix_g(nta, ntb, G_);
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
