@@ -2,8 +2,8 @@
 size-independent properties plus bounded oracle subsamples:
 
   * the normalised Gram restricted to a subset S equals the Gram of X[S] (pairs are independent:
-    the full-size launch must reproduce the small launch bit for bit up to fp32 rounding order,
-    here exactly, as each pair's recursion is the same instructions);
+    the full-size launch reproduces the small launch bit for bit where each pair's recursion is the
+    same instructions in any lane-group slot, and to fp32 rounding for the 10-lane groups);
   * symmetry, the constant normalised diagonal (sum of sigma * variances), positive semi-definiteness;
   * a subsample of rows against the float64 oracle (1e-5 norm-relative, the north_star bar)."""
 import numpy as np
@@ -37,7 +37,11 @@ def test_gram_full_size(cfg):
     S = np.unique(np.linspace(0, N - 1, 48).astype(int))
     St = torch.as_tensor(S, device=DEV)
     sub = K[St][:, St]
-    torch.testing.assert_close(sub, k.K(Xt[St]), rtol=0, atol=0)
+    # Aligned lane groups run every pair's recursion as the same instructions in any slot: bitwise.  The
+    # 10-lane groups at 65..100 points (C2) combine a scan's partial sums in an order that depends on where
+    # the group sits in the 16-lane DPP rows, so a pair moved to another slot differs by fp32 rounding.
+    seg = 64 < L <= 100
+    torch.testing.assert_close(sub, k.K(Xt[St]), rtol=0, atol=2e-6 if seg else 0)
     if N <= 1024:
         assert torch.linalg.eigvalsh(K.double()).min().item() > -1e-4
     # the symmetric oracle on a subset (K(X) and K(X, X2) differ on the diagonal by design: jitter
