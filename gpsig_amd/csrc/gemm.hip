@@ -14,6 +14,7 @@
 #include <hip/hip_runtime.h>
 
 #include "../../include/gpsig_amd.h"
+#include "gemm.h"
 
 namespace gpsig {
 
@@ -175,18 +176,24 @@ size_t gemm_splitk_bytes(int M, int N, int K) {
   return ks > 1 ? (size_t)ks * M * N * sizeof(float) : 0;
 }
 
-// C[b] = alpha op(A[b]) op(B[b]) + beta C[b] (row-major; transA / transB select op).  skip_rb/skip_cb > 0:
-// op(A) rows and op(B) columns come in blocks of skip_rb / skip_cb and the inputs vanish for row block >
-// column block (upper-triangle pair layouts): those output tiles are left untouched.
-// partial: a buffer of gemm_splitk_bytes(M, N, K) bytes lets an unbatched product split K (nullptr: no split)
+// see gemm.h
 int gemm_f32(hipStream_t s, bool transA, bool transB, int M, int N, int K, float alpha, const float *A,
              long long lda, long long sA, const float *B, long long ldb, long long sB, float beta, float *C,
-             long long ldc, long long sC, int batch, int skip_rb, int skip_cb, float *partial) {
+             long long ldc, long long sC, int batch, int skip_rb, int skip_cb, float *partial, size_t partial_bytes) {
   if (M <= 0 || N <= 0 || batch <= 0) return GPSIG_OK;
   if (K <= 0) return GPSIG_EINVAL;
-  const int ks = (batch == 1 && partial && skip_rb == 0) ? gemm_ksplit(M, N, K) : 1;
-  const int kc = ks > 1 ? (((K + ks - 1) / ks + GBK - 1) / GBK) * GBK : K;
-  const int nsl = ks > 1 ? (K + kc - 1) / kc : 1;
+  int ks = (batch == 1 && partial && skip_rb == 0) ? gemm_ksplit(M, N, K) : 1;
+  int kc = K, nsl = 1;
+  // the largest split (up to gemm_ksplit's) whose nsl partial products fit the caller's scratch
+  for (; ks > 1; --ks) {
+    kc = (((K + ks - 1) / ks + GBK - 1) / GBK) * GBK;
+    nsl = (K + kc - 1) / kc;
+    if (nsl > 1 && (size_t)nsl * (size_t)M * (size_t)N * sizeof(float) <= partial_bytes) break;
+  }
+  if (ks <= 1) {
+    kc = K;
+    nsl = 1;
+  }
   GemmArgs g{A, B, C, M, N, K, lda, ldb, ldc, sA, sB, sC, alpha, beta, skip_rb > 0 ? 1 : 0,
              skip_rb > 0 ? skip_rb : 1, skip_cb > 0 ? skip_cb : 1, nsl, kc, partial};
   dim3 grid((N + GBN - 1) / GBN, (M + GBM - 1) / GBM, nsl > 1 ? nsl : batch);
@@ -211,7 +218,7 @@ extern "C" int gpsig_gemm_f32(int transA, int transB, int M, int N, int K, float
                               gpsig_stream_t stream) {
   if (!A || !B || !C) return GPSIG_EINVAL;
   return gpsig::gemm_f32(reinterpret_cast<hipStream_t>(stream), transA != 0, transB != 0, M, N, K, alpha, A, lda, 0,
-                         B, ldb, 0, beta, C, ldc, 0, 1, 0, 0, nullptr);
+                         B, ldb, 0, beta, C, ldc, 0, 1, 0, 0, nullptr, 0);
 }
 
 // As gpsig_gemm_f32 with K split over partial products summed in a fixed order (workspace of
@@ -224,5 +231,6 @@ extern "C" int gpsig_gemm_f32_splitk(int transA, int transB, int M, int N, int K
   const size_t need = gpsig::gemm_splitk_bytes(M, N, K);
   if (need && (!workspace || workspace_bytes < need)) return GPSIG_EWORKSPACE;
   return gpsig::gemm_f32(reinterpret_cast<hipStream_t>(stream), transA != 0, transB != 0, M, N, K, alpha, A, lda, 0,
-                         B, ldb, 0, beta, C, ldc, 0, 1, 0, 0, need ? static_cast<float *>(workspace) : nullptr);
+                         B, ldb, 0, beta, C, ldc, 0, 1, 0, 0, need ? static_cast<float *>(workspace) : nullptr,
+                         need ? workspace_bytes : 0);
 }

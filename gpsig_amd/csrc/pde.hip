@@ -15,6 +15,7 @@
 //   solver 0: K[i+1][j+1] = K[i][j+1] + K[i+1][j] + K[i][j] (inc - 1)
 // In DIAG mode with solver 0 the diagonal cells take the solver-1 update, as sigKer_fast.pyx:59 does.
 #include "sig_common.h"
+#include "gemm.h"
 
 namespace gpsig {
 
@@ -567,9 +568,6 @@ int pde_launch(const float *X, int n1, int l1, const float *Y, int n2, int l2, i
 }
 
 // ------------------------------------------------------------------------------------ increment tiles
-int gemm_f32(hipStream_t s, bool transA, bool transB, int M, int N, int K, float alpha, const float *A, long long lda,
-             long long sA, const float *B, long long ldb, long long sB, float beta, float *C, long long ldc,
-             long long sC, int batch, int skip_rb, int skip_cb, float *partial);
 
 // dX[a][i][k] = x[a][i+1][k] - x[a][i][k]: the coarse increments, (n, l-1, d) row-major
 __global__ __launch_bounds__(256) void increments_kernel(const float *__restrict__ X, int n, int l, int d,
@@ -653,7 +651,7 @@ int pde_tiled_run(PdeArgs a, void *scratch, size_t scratch_bytes, hipStream_t s,
       c.inc_ld = IC;
       rc = gemm_f32(s, false, true, IC, IC, d, 1.0f, dX + (long long)c0 * IC * d, d, (long long)IC * d,
                     dX + (long long)c0 * IC * d, d, (long long)IC * d, 0.0f, T, IC, (long long)IC * IC, r1 - c0, 0, 0,
-                    nullptr);
+                    nullptr, 0);
     } else {
       const int b0 = pm == GPSIG_PAIRS_UPPER ? r0 : 0;
       const long long tc = (long long)(n2 - b0) * JC;
@@ -664,7 +662,7 @@ int pde_tiled_run(PdeArgs a, void *scratch, size_t scratch_bytes, hipStream_t s,
       // UPPER: tiles whose x-rows all lie past their y-columns are never read (b >= a)
       rc = gemm_f32(s, false, true, (r1 - r0) * IC, (int)tc, d, 1.0f, dX + (long long)r0 * IC * d, d, 0,
                     dY + (long long)b0 * JC * d, d, 0, 0.0f, T, tc, 0, 1, pm == GPSIG_PAIRS_UPPER ? IC : 0,
-                    pm == GPSIG_PAIRS_UPPER ? JC : 0, nullptr);
+                    pm == GPSIG_PAIRS_UPPER ? JC : 0, nullptr, 0);
     }
     if (rc) return rc;
     if ((rc = launch(c, s, ctx))) return rc;

@@ -1,15 +1,12 @@
 // gpsig_amd -- C ABI of the Goursat-PDE gradient (kernels in pde_bwd.h, one instantiation unit per
 // channel count: pde_bwd_inst.hip).
 #include "pde_bwd.h"
+#include "gemm.h"
 
 namespace gpsig {
 #define DECL(v) extern template int pde_bwd_launch_dp<v>(const PdeBwdArgs &, long long, int, hipStream_t);
 DECL(0) DECL(1) DECL(2) DECL(3) DECL(4) DECL(5) DECL(6) DECL(7) DECL(8) DECL(16)
 #undef DECL
-int gemm_f32(hipStream_t s, bool transA, bool transB, int M, int N, int K, float alpha, const float *A, long long lda,
-             long long sA, const float *B, long long ldb, long long sB, float beta, float *C, long long ldc,
-             long long sC, int batch, int skip_rb, int skip_cb, float *partial);
-size_t gemm_splitk_bytes(int M, int N, int K);
 int increments_launch(const float *X, int n, int l, int d, float *dX, hipStream_t s);
 
 // The adjoint on increment tiles: channel counts past the instantiations, dyadic orders past 3
@@ -38,8 +35,13 @@ static PdeBwdPlan pde_bwd_plan(int n1, int l1, int n2, int l2, int d, int pair_m
   p.gdy = p.dy;
   p.inc = al256b((size_t)r * IC * p.cols * sizeof(float));
   p.gt = p.inc;
-  const long long tiles = (r * IC + 127) / 128;
-  p.part = (rect && gemm_splitk_bytes((int)(r * IC), d, (int)p.cols)) ? al256b((size_t)(512 + tiles) * 128 * d * sizeof(float)) : 0;
+  // split-K partials of the two adjoint contractions of a full chunk (gdX: R x d, K = cols; gdY: cols x d,
+  // K = R); gemm_f32 clamps any split to this capacity
+  if (rect) {
+    const size_t pr = gemm_splitk_bytes((int)(r * IC), d, (int)p.cols);
+    const size_t pc = gemm_splitk_bytes((int)p.cols, d, (int)(r * IC));
+    p.part = al256b(pr > pc ? pr : pc);
+  }
   return p;
 }
 static size_t pde_bwd_plan_bytes(const PdeBwdPlan &p) { return p.dx + p.dy + p.gdx + p.gdy + p.inc + p.gt + p.part; }
@@ -68,7 +70,7 @@ extern "C" size_t gpsig_pde_vjp_scratch_bytes(int n1, int l1, int n2, int l2, in
 }
 
 extern "C" size_t gpsig_pde_vjp_workspace_bytes(int npairs, int l1, int l2, int dyadic) {
-  if (npairs <= 0 || l1 < 2 || l2 < 2 || dyadic < 0 || dyadic > 6) return 0;
+  if (npairs <= 0 || l1 < 2 || l2 < 2 || dyadic < 0 || dyadic > 8) return 0;
   return (size_t)npairs * (size_t)pde_front_floats(l1, l2, dyadic) * sizeof(float);
 }
 
@@ -118,7 +120,7 @@ static int pde_adj_tiled(PdeBwdArgs a, int mode, void *scratch, size_t scratch_b
       nblocks = (r1 - c0 + 3) / 4;
       rc = gemm_f32(s, false, true, IC, IC, d, 1.0f, dX + (long long)c0 * IC * d, d, (long long)IC * d,
                     dX + (long long)c0 * IC * d, d, (long long)IC * d, 0.0f, Tin, IC, (long long)IC * IC, r1 - c0, 0, 0,
-                    nullptr);
+                    nullptr, 0);
     } else {
       c.inc_a0 = r0;
       c.inc_b0 = 0;
@@ -128,7 +130,7 @@ static int pde_adj_tiled(PdeBwdArgs a, int mode, void *scratch, size_t scratch_b
       c.tiles_a0 = r0 / 4;
       nblocks = (long long)((r1 + 3) / 4 - r0 / 4) * n2;
       rc = gemm_f32(s, false, true, (r1 - r0) * IC, (int)pl.cols, d, 1.0f, dX + (long long)r0 * IC * d, d, 0, dY, d, 0,
-                    0.0f, Tin, pl.cols, 0, 1, 0, 0, nullptr);
+                    0.0f, Tin, pl.cols, 0, 1, 0, 0, nullptr, 0);
     }
     if (rc) return rc;
     if (nblocks > 0x7fffffffLL) return GPSIG_EUNSUPPORTED;
@@ -138,14 +140,14 @@ static int pde_adj_tiled(PdeBwdArgs a, int mode, void *scratch, size_t scratch_b
     if (!adj) continue;
     if (pm == GPSIG_PAIRS_DIAG) {
       rc = gemm_f32(s, false, false, IC, d, IC, 1.0f, Tg, IC, (long long)IC * IC, dX + (long long)c0 * IC * d, d,
-                    (long long)IC * d, 0.0f, gdX + (long long)c0 * IC * d, d, (long long)IC * d, r1 - c0, 0, 0, nullptr);
+                    (long long)IC * d, 0.0f, gdX + (long long)c0 * IC * d, d, (long long)IC * d, r1 - c0, 0, 0, nullptr, 0);
     } else {
       const int R = (r1 - r0) * IC;
       rc = gemm_f32(s, false, false, R, d, (int)pl.cols, 1.0f, Tg, pl.cols, 0, dY, d, 0, 1.0f,
-                    gdX + (long long)r0 * IC * d, d, 0, 1, 0, 0, part);
+                    gdX + (long long)r0 * IC * d, d, 0, 1, 0, 0, part, pl.part);
       if (!rc)
         rc = gemm_f32(s, true, false, (int)pl.cols, d, R, 1.0f, Tg, pl.cols, 0, dX + (long long)r0 * IC * d, d, 0, 1.0f,
-                      gdY, d, 0, 1, 0, 0, part);
+                      gdY, d, 0, 1, 0, 0, part, pl.part);
     }
     if (rc) return rc;
   }
@@ -169,7 +171,7 @@ static int pde_adj_impl(int mode, const float *X, int n1, int l1, const float *Y
                         size_t scratch_bytes = 0) {
   if (!X || !Y || n1 <= 0 || n2 <= 0 || d <= 0 || l1 < 2 || l2 < 2) return GPSIG_EINVAL;
   if (mode == 1 ? !out : (!gout || !gX)) return GPSIG_EINVAL;
-  if (dyadic < 0 || dyadic > 6 || (solver != 0 && solver != 1)) return GPSIG_EINVAL;
+  if (dyadic < 0 || dyadic > 8 || (solver != 0 && solver != 1)) return GPSIG_EINVAL;
   if (pair_mode != GPSIG_PAIRS_RECT && pair_mode != GPSIG_PAIRS_DIAG) return GPSIG_EINVAL;
   if (row_begin < 0 || row_end > n1 || row_begin > row_end) return GPSIG_EINVAL;
   if (pair_mode == GPSIG_PAIRS_DIAG && (n1 != n2 || l1 != l2 || X != Y)) return GPSIG_EINVAL;

@@ -3,13 +3,10 @@
 //   [gX | rowsum] += W [Y | 1],   [gY | colsum] += W^T [X | 1],   then  g -= rowsum * x  (RBF)
 // (UPPER / DIAG: Y = X, both sides go to gX).
 #include "sig_bwd_wide.h"
+#include "gemm.h"
 
 namespace gpsig {
 
-int gemm_f32(hipStream_t s, bool transA, bool transB, int M, int N, int K, float alpha, const float *A, long long lda,
-             long long sA, const float *B, long long ldb, long long sB, float beta, float *C, long long ldc,
-             long long sC, int batch, int skip_rb, int skip_cb, float *partial);
-size_t gemm_splitk_bytes(int M, int N, int K);
 template <int M>
 int sig_bwd_wide_launch_m(const BwdArgs &a, int seed, long long nblocks, hipStream_t s);
 bool ho_bwd_supported(int l2, int order, int M, int seed);
@@ -63,11 +60,13 @@ static WidePlan wide_plan(int n1, int l1, int n2, int l2, int d, int pair_mode) 
   p.gx = al256((size_t)n1 * l1 * (d + 1) * sizeof(float));
   p.gc = pair_mode == GPSIG_PAIRS_DIAG ? 0 : al256((size_t)n2 * l2 * (d + 1) * sizeof(float));
   p.tile = al256((size_t)rows * l1 * cols * sizeof(float));
-  // split-K partials of the row-side product (rows * l1 x (d + 1), K = cols): gemm_ksplit keeps
-  // ksplit * M <= (512 + tiles) * 128 for every chunk, the last (shorter) one included
-  const long long tiles = (rows * l1 + 127) / 128;
-  p.part = (pair_mode == GPSIG_PAIRS_DIAG || gemm_splitk_bytes((int)(rows * l1), d + 1, (int)cols) == 0)
-               ? 0 : al256((size_t)(512 + tiles) * 128 * (d + 1) * sizeof(float));
+  // split-K partials of the row-side (rows * l1 x (d + 1), K = cols) and column-side (cols x (d + 1),
+  // K = rows * l1) products of a full chunk; gemm_f32 clamps any split to this capacity
+  if (pair_mode != GPSIG_PAIRS_DIAG) {
+    const size_t pr = gemm_splitk_bytes((int)(rows * l1), d + 1, (int)cols);
+    const size_t pc = gemm_splitk_bytes((int)cols, d + 1, (int)(rows * l1));
+    p.part = al256(pr > pc ? pr : pc);
+  }
   return p;
 }
 
@@ -192,21 +191,21 @@ int sig_bwd_wide(BwdArgs a, const float *X, const float *Y, int seed, void *work
       const float *Xac = Xa + (long long)c0 * l1 * D1;
       // both sides of the pair (a, a): W X and W^T X, batched over the chunk's pairs
       if ((rc = gemm_f32(s, false, false, l1, D1, l1, 1.0f, T, l1, (long long)l1 * l1, Xac, D1, (long long)l1 * D1,
-                         0.0f, Gxc, D1, (long long)l1 * D1, na, 0, 0, nullptr)))
+                         0.0f, Gxc, D1, (long long)l1 * D1, na, 0, 0, nullptr, 0)))
         return rc;
       if ((rc = gemm_f32(s, true, false, l1, D1, l1, 1.0f, T, l1, (long long)l1 * l1, Xac, D1, (long long)l1 * D1,
-                         1.0f, Gxc, D1, (long long)l1 * D1, na, 0, 0, nullptr)))
+                         1.0f, Gxc, D1, (long long)l1 * D1, na, 0, 0, nullptr, 0)))
         return rc;
     } else {
       const int rows = nr * l1;
       const float *Bcols = (pm == GPSIG_PAIRS_UPPER ? Xa : Ya) + (long long)c.tile_b0 * l2 * D1;
       // row side: the chunk's rows of Gx
       if ((rc = gemm_f32(s, false, false, rows, D1, (int)tcols, 1.0f, T, tcols, 0, Bcols, D1, 0, 0.0f,
-                         Gx + (long long)r0 * l1 * D1, D1, 0, 1, 0, 0, part)))
+                         Gx + (long long)r0 * l1 * D1, D1, 0, 1, 0, 0, part, pl.part)))
         return rc;
       // column side: accumulated over the chunks
       if ((rc = gemm_f32(s, true, false, (int)tcols, D1, rows, 1.0f, T, tcols, 0, Xa + (long long)r0 * l1 * D1, D1,
-                         0, 1.0f, Gc + (long long)c.tile_b0 * l2 * D1, D1, 0, 1, 0, 0, part)))
+                         0, 1.0f, Gc + (long long)c.tile_b0 * l2 * D1, D1, 0, 1, 0, 0, part, pl.part)))
         return rc;
     }
   }

@@ -15,6 +15,7 @@
 // carry of the blocks to its left: per row, one float per scanned quantity (S00 and Sa[1..dn-1] of each
 // level), kept in this wave's LDS slab.
 #include "sig_common.h"
+#include "gemm.h"
 
 namespace gpsig {
 
@@ -325,9 +326,6 @@ int sig_ho_launch(const SigArgs &a, int DP, int seed, long long nblocks, hipStre
 void pde_tile_chunk(int n1, int l1, int n2, int l2, int pair_mode, int &rows, long long &cols);
 size_t pde_tile_scratch_bytes(int n1, int l1, int n2, int l2, int d, int pair_mode);
 int increments_launch(const float *X, int n, int l, int d, float *dX, hipStream_t s);
-int gemm_f32(hipStream_t s, bool transA, bool transB, int M, int N, int K, float alpha, const float *A, long long lda,
-             long long sA, const float *B, long long ldb, long long sB, float beta, float *C, long long ldc,
-             long long sC, int batch, int skip_rb, int skip_cb, float *partial);
 
 bool ho_tiled(int d, int order) { return order > 1 && d > 32; }
 size_t ho_tile_bytes(int n1, int l1, int n2, int l2, int d, int pair_mode) {
@@ -379,7 +377,7 @@ int sig_ho_tiled(SigArgs a, const float *X, const float *Y, int d, void *workspa
       nblocks = (r1 - c0 + 3) / 4;
       rc = gemm_f32(s, false, true, IC, IC, d, 1.0f, dX + (long long)c0 * IC * d, d, (long long)IC * d,
                     dX + (long long)c0 * IC * d, d, (long long)IC * d, 0.0f, T, IC, (long long)IC * IC, r1 - c0, 0, 0,
-                    nullptr);
+                    nullptr, 0);
     } else {
       const int b0 = pm == GPSIG_PAIRS_UPPER ? r0 : 0;
       const long long tc = (long long)(n2 - b0) * JC;
@@ -398,7 +396,7 @@ int sig_ho_tiled(SigArgs a, const float *X, const float *Y, int d, void *workspa
       }
       rc = gemm_f32(s, false, true, (r1 - r0) * IC, (int)tc, d, 1.0f, dX + (long long)r0 * IC * d, d, 0,
                     dY + (long long)b0 * JC * d, d, 0, 0.0f, T, tc, 0, 1, pm == GPSIG_PAIRS_UPPER ? IC : 0,
-                    pm == GPSIG_PAIRS_UPPER ? JC : 0, nullptr);
+                    pm == GPSIG_PAIRS_UPPER ? JC : 0, nullptr, 0);
     }
     if (rc) return rc;
     if (nblocks > 0x7fffffffLL) return GPSIG_EUNSUPPORTED;

@@ -12,13 +12,10 @@
 // then gX -= rowsum x, gZ0 -= colsum z0 (RBF).  Linear: gX += W^T Zw (w = z, or z1 - z0), gZ = W X
 // (increments: gZ1 += W X, gZ0 -= W X).
 #include "sig_common.h"
+#include "gemm.h"
 
 namespace gpsig {
 
-int gemm_f32(hipStream_t s, bool transA, bool transB, int M, int N, int K, float alpha, const float *A, long long lda,
-             long long sA, const float *B, long long ldb, long long sB, float beta, float *C, long long ldc,
-             long long sC, int batch, int skip_rb, int skip_cb, float *partial);
-size_t gemm_splitk_bytes(int M, int N, int K);
 size_t tvs_features_bytes(int n, int l, int d);
 int tvs_features_launch(const float *X, int n, int l, int d, float *Ft, hipStream_t s);
 
@@ -359,10 +356,8 @@ static TvswPlan tvsw_plan(int n, int l, int d, int lt, int t, bool incr) {
   p.w1 = incr ? p.w0 : 0;
   const size_t pa = gemm_splitk_bytes((int)(l * nc), d + 1, lt * t);
   const size_t pb = gemm_splitk_bytes(lt * t, d + 1, (int)(l * nc));
-  // the last chunk (fewer sequences) may split further: bound ksplit * M by (512 + tiles) * 128
-  const size_t ba = (size_t)(512 + (l * nc + 127) / 128) * 128 * (d + 1) * sizeof(float);
-  const size_t bb = (size_t)(512 + (lt * t + 127) / 128) * 128 * (d + 1) * sizeof(float);
-  p.part = a256((pa ? ba : 0) > (pb ? bb : 0) ? (pa ? ba : 0) : (pb ? bb : 0));
+  // gemm_f32 clamps the split of every chunk (the last, shorter one included) to this capacity
+  p.part = a256(pa > pb ? pa : pb);
   return p;
 }
 static size_t tvsw_bytes(const TvswPlan &p) { return p.ft + p.zw + p.za0 + p.za1 + p.xc + p.gxc + p.gz + p.w0 + p.w1 + p.part; }
@@ -399,7 +394,7 @@ int tvs_bwd_wide(const float *Z, int lt, int t, int incr, int d, const float *X,
   float *Gz = reinterpret_cast<float *>(w); w += pl.gz;
   float *W0 = reinterpret_cast<float *>(w); w += pl.w0;
   float *W1 = pl.w1 ? reinterpret_cast<float *>(w) : nullptr; w += pl.w1;
-  float *part = reinterpret_cast<float *>(w);
+  float *part = pl.part ? reinterpret_cast<float *>(w) : nullptr;
   int rc = tvs_features_launch(X, n, l, d, Ft, s);
   if (rc) return rc;
   const long long zr = (long long)lt * t;
@@ -431,18 +426,18 @@ int tvs_bwd_wide(const float *Z, int lt, int t, int incr, int d, const float *X,
     if (rc) return rc;
     const int R = l * nc;
     // sequence side: the chunk's point gradients, rows (s, j)
-    if ((rc = gemm_f32(s, true, false, R, D1, (int)zr, 1.0f, W0, R, 0, Za0, D1, 0, 0.0f, Gxc, D1, 0, 1, 0, 0, part)))
+    if ((rc = gemm_f32(s, true, false, R, D1, (int)zr, 1.0f, W0, R, 0, Za0, D1, 0, 0.0f, Gxc, D1, 0, 1, 0, 0, part, pl.part)))
       return rc;
-    if (Gz1 && (rc = gemm_f32(s, true, false, R, D1, (int)zr, 1.0f, W1, R, 0, Za1, D1, 0, 1.0f, Gxc, D1, 0, 1, 0, 0, part)))
+    if (Gz1 && (rc = gemm_f32(s, true, false, R, D1, (int)zr, 1.0f, W1, R, 0, Za1, D1, 0, 1.0f, Gxc, D1, 0, 1, 0, 0, part, pl.part)))
       return rc;
     hipLaunchKernelGGL(tvsw_gx_kernel, dim3((unsigned)(((long long)R * d + 255) / 256)), dim3(256), 0, s, Gxc, X, l, d,
                        n0, nc, rbf ? 1 : 0, gX);
     // tensor side: [gZ | colsum] += W [X | 1] over the chunk's points
     hipLaunchKernelGGL(tvsw_points_kernel, dim3((unsigned)(((long long)R * D1 + 255) / 256)), dim3(256), 0, s, X, l, d,
                        n0, nc, Xc);
-    if ((rc = gemm_f32(s, false, false, (int)zr, D1, R, 1.0f, W0, R, 0, Xc, D1, 0, 1.0f, Gz0, D1, 0, 1, 0, 0, part)))
+    if ((rc = gemm_f32(s, false, false, (int)zr, D1, R, 1.0f, W0, R, 0, Xc, D1, 0, 1.0f, Gz0, D1, 0, 1, 0, 0, part, pl.part)))
       return rc;
-    if (Gz1 && (rc = gemm_f32(s, false, false, (int)zr, D1, R, 1.0f, W1, R, 0, Xc, D1, 0, 1.0f, Gz1, D1, 0, 1, 0, 0, part)))
+    if (Gz1 && (rc = gemm_f32(s, false, false, (int)zr, D1, R, 1.0f, W1, R, 0, Xc, D1, 0, 1.0f, Gz1, D1, 0, 1, 0, 0, part, pl.part)))
       return rc;
   }
   // gZ: RBF z0 (and z1) with the colsum correction; linear: w = z (or z1 - z0: +z1, -z0)

@@ -263,7 +263,8 @@ int gpsig_pde_diag_ex(const float *X, int n, int l, int d, int dyadic, int solve
  * I = 2^dyadic (l1-1), J = 2^dyadic (l2-1)), gpsig_pde_vjp_workspace_bytes(pairs, l1, l2, dyadic), which
  * returns 0 where the kernel does not apply.  Wider grids than one wave's 64 W columns are swept in column
  * blocks; their fp64 boundary columns are part of the workspace.  Past dyadic 3 (and past 16 channels) the
- * _ex entries below apply (the fronts then follow the grid refined 2^(dyadic - 3) per tile cell). */
+ * _ex entries below apply (the fronts then follow the grid refined 2^(dyadic - 3) per tile cell).  dyadic <= 8,
+ * as the forward. */
 size_t gpsig_pde_vjp_workspace_bytes(int npairs, int l1, int l2, int dyadic);
 
 int gpsig_pde_vjp(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int dyadic, int solver,

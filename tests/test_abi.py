@@ -92,7 +92,8 @@ def test_vjp_and_feature_entry_points_validate_arguments():
     assert lib.gpsig_pde_vjp_workspace_bytes(2, 10, 1100, 0) == 2 * (2 * 36 * 17 * 64 + 2 * 2 * 10) * 4
     # dyadic > 3: the order-3 layout of the grid whose cells are split 2^(dyadic-3) (tile sub-refinement)
     assert lib.gpsig_pde_vjp_workspace_bytes(2, 10, 10, 4) == lib.gpsig_pde_vjp_workspace_bytes(2, 19, 19, 3)
-    assert lib.gpsig_pde_vjp_workspace_bytes(2, 10, 10, 7) == 0
+    assert lib.gpsig_pde_vjp_workspace_bytes(2, 10, 10, 7) == lib.gpsig_pde_vjp_workspace_bytes(2, 145, 145, 3)
+    assert lib.gpsig_pde_vjp_workspace_bytes(2, 10, 10, 9) == 0
 
 
 def test_graph_capture_refuses_host_tensors_and_kernel_to():

@@ -94,3 +94,50 @@ def test_pde_tiled_fronts_and_autograd(d, n):
     torch.testing.assert_close(Kg.detach(), kp.K(Xf.detach()), rtol=1e-7, atol=0)
     (Kg * torch.randn(5, 5, device=DEV, dtype=torch.float64)).sum().backward()
     assert torch.isfinite(Xf.grad).all()
+
+
+@pytest.mark.parametrize("n", [6, 7, 8])
+def test_pde_dyadic_6_to_8_forward_and_vjp(n):
+    """The forward's dyadic cap (8) is the adjoint's too: dyadic 6-8 forward (tile cells split 2^(n-4) ways)
+    and the adjoint on the REP-8 layout (cells split 2^(n-3) ways) against the C oracle; autograd through
+    UntruncSignatureKernel.K at the same order."""
+    import gpsig_amd
+    from gpsig_amd import ops
+    rng = np.random.default_rng(600 + n)
+    L, d = 9, 3
+    X, Y = paths(rng, 2, L, d), paths(rng, 2, L - 1, d)
+    Xt, Yt = torch.tensor(X, device=DEV), torch.tensor(Y, device=DEV)
+    got = ops.pde_gram(Xt, Yt, n, 1).cpu().numpy()
+    assert norm_rel_err(got, pde.pde_gram(X, Y, n, 1)) < TOL
+    kd = ops.pde_diag(Xt, n, 1).cpu().numpy()
+    exp = pde.pde_diag(X, n, 1)
+    assert np.abs(kd - exp).max() / np.abs(exp).max() < TOL
+    G = rng.standard_normal((2, 2))
+    gX, gY = ops.pde_gram_vjp(Xt.float(), Yt.float(), torch.tensor(G, device=DEV, dtype=torch.float32), n, 1)
+    rx, ry = pde.pde_gram_grad(X, Y, G, n, 1)
+    assert norm_rel_err(gX.cpu().numpy(), rx) < TOL
+    assert norm_rel_err(gY.cpu().numpy(), ry) < TOL
+    kp = gpsig_amd.UntruncSignatureKernel(L * d, d, order=n)
+    Xf = Xt.reshape(2, -1).double().requires_grad_(True)
+    kp.K(Xf).sum().backward()
+    assert torch.isfinite(Xf.grad).all()
+
+
+def test_pde_tiled_vjp_column_side_split_k():
+    """Tiled adjoint with n2 (l2 - 1) >> rows per chunk: the dLoss/d dy contraction (M = n2 (l2 - 1), K = the
+    chunk's rows) splits K and must stay inside the scratch (gemm_f32 clamps the split).  The loss weights
+    three y-paths only, so the C oracle runs on those; the other y-gradients must be exactly zero."""
+    from gpsig_amd import ops
+    rng = np.random.default_rng(64)
+    n1, n2, L, d = 64, 1000, 64, 32
+    X, Y = paths(rng, n1, L, d), paths(rng, n2, L, d)
+    sel = [0, 500, 999]
+    G = np.zeros((n1, n2))
+    G[:, sel] = rng.standard_normal((n1, len(sel)))
+    f = lambda v: torch.tensor(v, device=DEV, dtype=torch.float32)
+    gX, gY = ops.pde_gram_vjp(f(X), f(Y), f(G), 0, 1)
+    rx, ry = pde.pde_gram_grad(X, Y[sel], G[:, sel], 0, 1)
+    assert norm_rel_err(gX.cpu().numpy(), rx) < TOL
+    gy = gY.cpu().numpy()
+    assert norm_rel_err(gy[sel], ry) < TOL
+    assert not np.any(np.delete(gy, sel, axis=0))

@@ -393,3 +393,28 @@ def test_tile_paths_row_windows(path):
         got = part(r0, r1)
         for a in range(r0, r1):
             torch.testing.assert_close(got[:, a - r0, a:], full[:, a, a:], rtol=1e-6, atol=1e-7)
+
+
+def test_wide_vjp_column_side_split_k():
+    """RECT VJP with far more column-side points than one row chunk holds (n2 * l2 >> rows * l1): the
+    column-side emission GEMM splits K on its own, and its partial products must stay inside the workspace
+    (gemm_f32 clamps the split to the capacity it is given).  The loss weights only four y-sequences, so the
+    fp64 oracle runs on those; every other y-gradient must be exactly zero."""
+    from gpsig_amd import ops
+    from oracle import autodiff_ref as ar
+    rng = np.random.default_rng(400)
+    N1, N2, L, D, M = 8, 400, 100, 32, 2
+    X = walks(rng, N1, L, D)
+    Y = walks(rng, N2, L, D)
+    sel = [0, 1, 398, 399]
+    G = np.zeros((M + 1, N1, N2))
+    G[:, :, sel] = rng.standard_normal((M + 1, N1, len(sel)))
+    gX, gY = ops.sig_gram_vjp(t(X).float(), t(Y).float(), M, t(G).float(), gout_levels=True)
+    Xr = torch.tensor(X, requires_grad=True)
+    Yr = torch.tensor(Y[sel], requires_grad=True)
+    (ar.k_seq(Xr, Yr, M, "rbf") * torch.tensor(G[:, :, sel])).sum().backward()
+    assert norm_rel_err(gX.cpu().numpy(), Xr.grad.numpy()) < GTOL
+    gy = gY.cpu().numpy()
+    assert norm_rel_err(gy[sel], Yr.grad.numpy()) < GTOL
+    rest = np.setdiff1d(np.arange(N2), sel)
+    assert not np.any(gy[rest])
