@@ -13,7 +13,7 @@ size_t fo_split_bytes(int l1, int l2, int DP, int M);
 int sig_ho_launch(const SigArgs &a, int DP, int seed, long long nblocks, hipStream_t s);
 bool ho_tiled(int d, int order);
 size_t ho_tile_bytes(int n1, int l1, int n2, int l2, int d, int pair_mode);
-int sig_ho_tiled(SigArgs a, const float *X, const float *Y, int d, void *workspace, size_t workspace_bytes,
+int sig_ho_tiled(SigArgs a, const float *X, const float *Y, int d, int seed, void *workspace, size_t workspace_bytes,
                  hipStream_t s);
 int ho_lanes_per_pair(int l2, int order, int M);
 int pde_launch(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int dyadic, int solver,
@@ -22,6 +22,11 @@ int pde_launch(const float *X, int n1, int l1, const float *Y, int n2, int l2, i
 int sym_assemble_launch(const float *src, const long long *row_off, long long level_stride, int n, int levels,
                         float *dst, hipStream_t s);
 bool pde_tiled(int d, int dyadic);
+int mf_records(const float *X, int n, int l, int d, float *R, hipStream_t s);
+size_t mf_records_bytes(int n, int l, int d);
+bool mf_gram_applies(int d, int l2);
+size_t mf_gram_scratch_bytes(int l1, int l2, int d);
+int sig_fo_mf(const SigArgs &a, int d, int seed, float *scratch, hipStream_t s);
 size_t pde_tile_scratch_bytes(int n1, int l1, int n2, int l2, int d, int pair_mode);
 int pde_launch_tiled(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int dyadic, int solver,
                      int pair_mode, int row_begin, int row_end, float *out, int out_row0, int out_rows,
@@ -59,8 +64,22 @@ int fo_fixed_max() {
 }  // namespace gpsig
 static bool wide_channels(int d, int order) { return order == 1 && d > fo_fixed_max(); }
 
+// The wide-channel Gram with the increment GEMM on the matrix cores (sig_fo_mf.h) for the difference seeds
+// of the Gram pair modes; GPSIG_WIDE_MF=0 keeps the runtime-channel-loop kernel (A/B runs).
+namespace gpsig {
+bool wide_mf_enabled() {
+  static const bool v = [] {
+    const char *e = getenv("GPSIG_WIDE_MF");
+    return !(e && atoi(e) == 0);
+  }();
+  return v;
+}
+}  // namespace gpsig
+
 static size_t feat_bytes(int n, int l, int d) {
-  const size_t wb = d > fo_fixed_max() ? align256((size_t)n * wide_rec_floats(d, l) * sizeof(float)) : 0;
+  size_t wb = d > fo_fixed_max() ? align256((size_t)n * wide_rec_floats(d, l) * sizeof(float)) : 0;
+  const size_t mb = d > fo_fixed_max() ? align256(mf_records_bytes(n, l, d)) : 0;
+  wb = mb > wb ? mb : wb;
   const int DP = pad_channels(d, 2);  // the wider of the two paddings
   const size_t fb = DP ? align256((size_t)n * l * feat_stride(DP) * sizeof(float)) : 0;
   return wb > fb ? wb : fb;
@@ -72,8 +91,13 @@ static int seed_of(int base_kind, int difference) {
   return -1;
 }
 
+// the matrix-core wide Gram's column-block carries (sequences past 160 points), after the records
+static size_t mf_scratch(int l1, int l2, int d) {
+  return d > fo_fixed_max() && wide_mf_enabled() ? align256(mf_gram_scratch_bytes(l1, l2, d)) : 0;
+}
+
 extern "C" size_t gpsig_sig_workspace_bytes(int n1, int l1, int n2, int l2, int d) {
-  return feat_bytes(n1, l1, d) + feat_bytes(n2, l2, d);
+  return feat_bytes(n1, l1, d) + feat_bytes(n2, l2, d) + mf_scratch(l1, l2, d);
 }
 
 // The workspace of one gpsig_sig_gram / gpsig_sig_diag call: the feature records, or for the higher-order
@@ -114,7 +138,7 @@ static int sig_gram_impl(const float *X, int n1, int l1, const float *Y, int n2,
   if (split && (mfma || seed != SEED_RBF_DIFF || order != 1 || state || pair_mode == GPSIG_PAIRS_DIAG))
     return GPSIG_EUNSUPPORTED;
   const bool tiled = ho_tiled(d, order);  // higher order past 32 channels: cells from an increment-Gram tile
-  if (tiled && (seed != SEED_LIN_DIFF || mfma || split || state)) return GPSIG_EUNSUPPORTED;
+  if (tiled && ((seed != SEED_LIN_DIFF && seed != SEED_RBF_DIFF) || mfma || split || state)) return GPSIG_EUNSUPPORTED;
   const bool wide = wide_channels(d, order);
   const int DP = (wide || tiled) ? 0 : pad_channels(d, order);
   if (seed < 0 || (DP == 0 && !wide && !tiled)) return GPSIG_EUNSUPPORTED;
@@ -136,20 +160,25 @@ static int sig_gram_impl(const float *X, int n1, int l1, const float *Y, int n2,
     a.out_rows = out_rows;
     a.out_ld = n2;
     a.out_lvl = pair_mode == GPSIG_PAIRS_DIAG ? (long long)n1 : (long long)out_rows * n2;
-    return sig_ho_tiled(a, X, Y, d, workspace, workspace_bytes, s);
+    return sig_ho_tiled(a, X, Y, d, seed, workspace, workspace_bytes, s);
   }
 
   const bool same = (X == Y && n1 == n2 && l1 == l2);
+  const bool mf = wide && wide_mf_enabled() && pair_mode != GPSIG_PAIRS_DIAG &&
+                  (seed == SEED_RBF_DIFF || seed == SEED_LIN_DIFF) && mf_gram_applies(d, l2);
   const size_t fx_b = wide ? feat_bytes(n1, l1, d) : align256((size_t)n1 * l1 * feat_stride(DP) * sizeof(float));
   const size_t fy_b = same ? 0 : (wide ? feat_bytes(n2, l2, d) : align256((size_t)n2 * l2 * feat_stride(DP) * sizeof(float)));
   const size_t dm_b = split ? gpsig_sig_split_bytes(l1, l2, d, num_levels) : 0;
   if (split && dm_b == 0) return GPSIG_EUNSUPPORTED;
-  if (!workspace || workspace_bytes < fx_b + fy_b + dm_b) return GPSIG_EWORKSPACE;
+  const size_t mc_b = mf ? mf_scratch(l1, l2, d) : 0;
+  if (!workspace || workspace_bytes < fx_b + fy_b + dm_b + mc_b) return GPSIG_EWORKSPACE;
   float *FX = static_cast<float *>(workspace);
   float *FY = same ? FX : reinterpret_cast<float *>(static_cast<char *>(workspace) + fx_b);
-  int rc = wide ? wide_records(X, n1, l1, d, FX, s) : features(X, n1, l1, d, DP, FX, s);
+  int rc = mf ? mf_records(X, n1, l1, d, FX, s) : wide ? wide_records(X, n1, l1, d, FX, s) : features(X, n1, l1, d, DP, FX, s);
   if (rc) return rc;
-  if (!same && (rc = wide ? wide_records(Y, n2, l2, d, FY, s) : features(Y, n2, l2, d, DP, FY, s))) return rc;
+  if (!same && (rc = mf ? mf_records(Y, n2, l2, d, FY, s)
+                        : wide ? wide_records(Y, n2, l2, d, FY, s) : features(Y, n2, l2, d, DP, FY, s)))
+    return rc;
 
   SigArgs a{};
   a.FX = FX;
@@ -177,6 +206,8 @@ static int sig_gram_impl(const float *X, int n1, int l1, const float *Y, int n2,
   a.lw2 = wide_lw(l2);
   a.sx = wide_rec_floats(d, l1);
   a.sy = wide_rec_floats(d, l2);
+  if (mf)
+    return sig_fo_mf(a, d, seed, mc_b ? reinterpret_cast<float *>(static_cast<char *>(workspace) + fx_b + fy_b) : nullptr, s);
 
   const int LP = (order == 1) ? fo_lanes_per_pair(l2, DP, num_levels, mfma, seed, split) : ho_lanes_per_pair(l2, order, num_levels);
   if (LP == 0) return GPSIG_EUNSUPPORTED;

@@ -73,38 +73,55 @@ GPSIG_DEV void group_incl_scan_n(float (&v)[N]) {
 
 // Lane groups that are not aligned to DPP rows: LP = 10 or 20 lanes per group, groups at lanes 0, LP,
 // 2 LP, ... (64 / LP of them; the remaining lanes form a partial group whose results are discarded).
-// Every such group spans at most two 16-lane rows (group starts fall at row offsets 0, 10, 4, 14, 8, 2
-// for LP = 10 and 0, 4, 8 for LP = 20), so a segmented Hillis-Steele scan needs the four in-row steps
-// (row_shr, whose out-of-row sources read 0) with the term weighted by a per-lane 0/1 factor (source in
-// the same group: gl >= s), plus one row_bcast:15 step taken by the lanes whose group began in the
-// previous row (lane 15 of that row then holds the group's sum from its start).  Five DPP steps, as
-// the LP = 32 scan.
+// Such a group straddles a 16-lane DPP row at a position that depends on its slot (row offsets 0, 10, 4, 14,
+// 8, 2 for LP = 10), and a DPP scan (row_shr inside rows, row_bcast across them) would then combine the
+// partial sums in a slot-dependent order: a pair moved to another slot would differ by fp32 rounding.  So the
+// scan is a plain Hillis-Steele scan over the whole wave, every step reading lane - s through ds_bpermute
+// (the LDS crossbar; no LDS storage, no VALU issue), its term weighted by a per-lane 0/1 factor (source in
+// the same group: gl >= s).  Every lane of every group then evaluates the same tree,
+//   S_1(gl) = v(gl) + v(gl-1),  S_2(gl) = S_1(gl) + S_1(gl-2),  ...,
+// so results are bitwise independent of the slot (K(X)[S, S] == K(X[S])).
 template <int LP>
 struct SegFactors {
-  float f1, f2, f4, f8, fb;
+  static constexpr int NS = LP > 16 ? 5 : 4;  // steps 1, 2, 4, 8 (, 16)
+  float f[NS];
+  int base;  // 4 lane: ds_bpermute takes address bits [7:2], so base + 256 - 4 s addresses lane - s mod 64
+             // (the constant folds into the instruction's offset; wrapped sources are masked)
   GPSIG_DEV SegFactors() {
-    const int lane = (int)__lane_id(), gl = lane % LP, rl = lane & 15;
-    f1 = gl >= 1 ? 1.0f : 0.0f;
-    f2 = gl >= 2 ? 1.0f : 0.0f;
-    f4 = gl >= 4 ? 1.0f : 0.0f;
-    f8 = gl >= 8 ? 1.0f : 0.0f;
-    fb = gl > rl ? 1.0f : 0.0f;
+    const int lane = (int)__lane_id(), gl = lane % LP;
+    base = 4 * lane;
+#pragma unroll
+    for (int t = 0; t < NS; ++t) f[t] = gl >= (1 << t) ? 1.0f : 0.0f;
   }
 };
+// v[k] from lane - S (mod 64) for N values: ds_bpermute with the shift in the instruction's offset field (the
+// compiler materialises a register per constant address otherwise), one lgkmcnt wait for the batch.
+template <int S, int N>
+GPSIG_DEV void bperm_sub_n(int base, const float (&v)[N], float (&u)[N]) {
+  constexpr int OFF = 256 - 4 * S;
+#pragma unroll
+  for (int k = 0; k < N; ++k)
+    asm volatile("ds_bpermute_b32 %0, %1, %2 offset:%3" : "=v"(u[k]) : "v"(base), "v"(v[k]), "i"(OFF));
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  // the results exist only after the wait: tie every later use to it (volatile asm keeps this order)
+#pragma unroll
+  for (int k = 0; k < N; ++k) asm volatile("" : "+v"(u[k]));
+}
 template <int LP, int N>
 GPSIG_DEV void seg_incl_scan_n(float (&v)[N], const SegFactors<LP> &f) {
   static_assert(LP == 10 || LP == 20, "segmented groups");
-#pragma unroll
-  for (int k = 0; k < N; ++k) v[k] = __builtin_fmaf(dpp_f<0x111>(v[k]), f.f1, v[k]);
-#pragma unroll
-  for (int k = 0; k < N; ++k) v[k] = __builtin_fmaf(dpp_f<0x112>(v[k]), f.f2, v[k]);
-#pragma unroll
-  for (int k = 0; k < N; ++k) v[k] = __builtin_fmaf(dpp_f<0x114>(v[k]), f.f4, v[k]);
-#pragma unroll
-  for (int k = 0; k < N; ++k) v[k] = __builtin_fmaf(dpp_f<0x118>(v[k]), f.f8, v[k]);
-#pragma unroll
-  for (int k = 0; k < N; ++k) v[k] = __builtin_fmaf(dpp_f<0x142>(v[k]), f.fb, v[k]);
+  float u[N];
+#define GPSIG_SEG_STEP(t)                                                         \
+  bperm_sub_n<(1 << t), N>(f.base, v, u);                                         \
+  _Pragma("unroll") for (int k = 0; k < N; ++k) v[k] = __builtin_fmaf(u[k], f.f[t], v[k]);
+  GPSIG_SEG_STEP(0)
+  GPSIG_SEG_STEP(1)
+  GPSIG_SEG_STEP(2)
+  GPSIG_SEG_STEP(3)
+  if constexpr (SegFactors<LP>::NS > 4) { GPSIG_SEG_STEP(4) }
+#undef GPSIG_SEG_STEP
 }
+
 // Sum over a segmented group (LP = 10 / 20), valid in the group's first lane (gl == 0).
 template <int LP>
 GPSIG_DEV float seg_group_sum(float v, const SegFactors<LP> &f) {

@@ -53,6 +53,7 @@ struct SigArgs {
   long long tile_as, tile_ld;
   int tile_a0, tile_b0;
   const float *RX, *RY;
+  int tile_rbf;  // the tile holds RBF difference-seed cells (level 1 closed form of the RBF kernel)
 };
 
 // Saved forward state of a first-order pair (gpsig_sig_gram_state): column sums of levels 1..M-1

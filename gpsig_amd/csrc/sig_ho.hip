@@ -244,14 +244,27 @@ __global__ __launch_bounds__(256) void sig_ho_kernel(SigArgs p) {
 #pragma unroll
   for (int m = 1; m <= MMAX; ++m) K[m] = Kacc[m];
   if constexpr (TILE) {
-    // level 1 in closed form, sum_ij <dx_i, dy_j> = <x_L - x_0, y_L - y_0> (fp64, channels over the lanes)
+    // level 1 in closed form (fp64, channels over the lanes): linear sum_ij <dx_i, dy_j> = <x_L - x_0, y_L - y_0>,
+    // RBF cells (tile_rbf) the corner difference k(x_L, y_L) - k(x_L, y_0) - k(x_0, y_L) + k(x_0, y_0)
     const int d = p.wd;
     const float *xa = p.RX + (long long)a * p.l1 * d, *yb = p.RY + (long long)b * p.l2 * d;
-    double s = 0.0;
-    for (int k = lane; k < d; k += 64)
-      s += ((double)xa[(long long)(p.l1 - 1) * d + k] - (double)xa[k]) * ((double)yb[(long long)(p.l2 - 1) * d + k] - (double)yb[k]);
-    for (int o = 32; o >= 1; o >>= 1) s += __shfl_xor(s, o, 64);
-    K[1] = (float)s;
+    const float *xl = xa + (long long)(p.l1 - 1) * d, *yl = yb + (long long)(p.l2 - 1) * d;
+    double s[4] = {0.0, 0.0, 0.0, 0.0};
+    for (int k = lane; k < d; k += 64) {
+      const double x0 = xa[k], x1 = xl[k], y0 = yb[k], y1 = yl[k];
+      if (p.tile_rbf) {
+        s[0] += (x0 - y0) * (x0 - y0);
+        s[1] += (x0 - y1) * (x0 - y1);
+        s[2] += (x1 - y0) * (x1 - y0);
+        s[3] += (x1 - y1) * (x1 - y1);
+      } else {
+        s[0] += (x1 - x0) * (y1 - y0);
+      }
+    }
+    for (int o = 32; o >= 1; o >>= 1)
+      for (int u = 0; u < 4; ++u) s[u] += __shfl_xor(s[u], o, 64);
+    K[1] = p.tile_rbf ? (float)((exp(-0.5 * s[3]) - exp(-0.5 * s[2])) - (exp(-0.5 * s[1]) - exp(-0.5 * s[0])))
+                      : (float)s[0];
   }
   if (lane == 0) {
     if constexpr (!TILE) K[1] = level1_closed<DP, SEED>(fx, fy, p.l1, p.l2);  // ho seeds are the DIFF seeds
@@ -327,15 +340,35 @@ void pde_tile_chunk(int n1, int l1, int n2, int l2, int pair_mode, int &rows, lo
 size_t pde_tile_scratch_bytes(int n1, int l1, int n2, int l2, int d, int pair_mode);
 int increments_launch(const float *X, int n, int l, int d, float *dX, hipStream_t s);
 
+int mf_records(const float *X, int n, int l, int d, float *R, hipStream_t s);
+size_t mf_records_bytes(int n, int l, int d);
+bool mf_gram_applies(int d, int l2);
+int sig_fo_mf_cells(const float *FX, int n1, int l1, const float *FY, int n2, int l2, int d, int pair_mode,
+                    int row_begin, int row_end, float *dm, int dm_a0, int dm_b0, long long dm_as, long long dm_bs,
+                    long long dm_ld, hipStream_t s);
+
 bool ho_tiled(int d, int order) { return order > 1 && d > 32; }
+static size_t al256h(size_t b) { return (b + 255) & ~(size_t)255; }
+// the operands of a chunk's cells (linear: the increments; RBF: the matrix-core seed's records), then the tile
+static size_t ho_operand_bytes(int n1, int l1, int n2, int l2, int d, int pair_mode) {
+  const bool rect = pair_mode == GPSIG_PAIRS_RECT;
+  const size_t inc = al256h((size_t)n1 * (l1 - 1) * d * sizeof(float)) + (rect ? al256h((size_t)n2 * (l2 - 1) * d * sizeof(float)) : 0);
+  const size_t rec = al256h(mf_records_bytes(n1, l1, d)) + (rect ? al256h(mf_records_bytes(n2, l2, d)) : 0);
+  return inc > rec ? inc : rec;
+}
 size_t ho_tile_bytes(int n1, int l1, int n2, int l2, int d, int pair_mode) {
-  return pde_tile_scratch_bytes(n1, l1, n2, l2, d, pair_mode);
+  if (n1 <= 0 || n2 <= 0 || l1 < 2 || l2 < 2 || d <= 0) return 0;
+  int rows;
+  long long cols;
+  pde_tile_chunk(n1, l1, n2, l2, pair_mode, rows, cols);
+  return ho_operand_bytes(n1, l1, n2, l2, d, pair_mode) + al256h((size_t)rows * (l1 - 1) * cols * sizeof(float));
 }
 static inline long long ho_upper_prefix(long long r, long long ntb) { return r * ntb - 4 * r * (r - 1) / 2; }
 
-// Chunks of x-rows: the increment tile of the chunk (one matrix-core GEMM dX_chunk dY^T, batched per pair
-// for DIAG), then the tile-fed recursion.  a: filled by the caller (rows, mode, output, M, order).
-int sig_ho_tiled(SigArgs a, const float *X, const float *Y, int d, void *workspace, size_t workspace_bytes,
+// Chunks of x-rows: the cell tile of the chunk -- linear: the increment Gram (one matrix-core GEMM dX_chunk dY^T,
+// batched per pair for DIAG); RBF: the difference-seed cells from the matrix-core wide seed (sig_fo_mf.h, cell
+// producer) -- then the tile-fed recursion.  a: filled by the caller (rows, mode, output, M, order).
+int sig_ho_tiled(SigArgs a, const float *X, const float *Y, int d, int seed, void *workspace, size_t workspace_bytes,
                  hipStream_t s) {
   const int n1 = a.n1, l1 = a.l1, n2 = a.n2, l2 = a.l2, pm = a.pair_mode;
   const int IC = l1 - 1, JC = l2 - 1;
@@ -344,20 +377,19 @@ int sig_ho_tiled(SigArgs a, const float *X, const float *Y, int d, void *workspa
   int rows;
   long long cols;
   pde_tile_chunk(n1, l1, n2, l2, pm, rows, cols);
+  const bool rbf = seed == SEED_RBF_DIFF;
+  if (rbf ? !mf_gram_applies(d, l2) : seed != SEED_LIN_DIFF) return GPSIG_EUNSUPPORTED;
   char *w = static_cast<char *>(workspace);
-  auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
-  float *dX = reinterpret_cast<float *>(w);
-  w += al((size_t)n1 * IC * d * sizeof(float));
-  float *dY = dX;
-  if (pm == GPSIG_PAIRS_RECT) {
-    dY = reinterpret_cast<float *>(w);
-    w += al((size_t)n2 * JC * d * sizeof(float));
-  }
-  float *T = reinterpret_cast<float *>(w);
-  int rc = increments_launch(X, n1, l1, d, dX, s);
+  float *dX = reinterpret_cast<float *>(w), *dY = dX;
+  const size_t xb = rbf ? al256h(mf_records_bytes(n1, l1, d)) : al256h((size_t)n1 * IC * d * sizeof(float));
+  if (pm == GPSIG_PAIRS_RECT) dY = reinterpret_cast<float *>(w + xb);
+  float *T = reinterpret_cast<float *>(w + ho_operand_bytes(n1, l1, n2, l2, d, pm));
+  int rc = rbf ? mf_records(X, n1, l1, d, dX, s) : increments_launch(X, n1, l1, d, dX, s);
   if (rc) return rc;
-  if (pm == GPSIG_PAIRS_RECT && (rc = increments_launch(Y, n2, l2, d, dY, s))) return rc;
+  if (pm == GPSIG_PAIRS_RECT && (rc = rbf ? mf_records(Y, n2, l2, d, dY, s) : increments_launch(Y, n2, l2, d, dY, s)))
+    return rc;
   a.tile = T;
+  a.tile_rbf = rbf ? 1 : 0;
   a.RX = X;
   a.RY = pm == GPSIG_PAIRS_RECT ? Y : X;
   a.wd = d;
@@ -375,9 +407,12 @@ int sig_ho_tiled(SigArgs a, const float *X, const float *Y, int d, void *workspa
       c.tile_as = (long long)IC * IC;
       c.tile_ld = IC;
       nblocks = (r1 - c0 + 3) / 4;
-      rc = gemm_f32(s, false, true, IC, IC, d, 1.0f, dX + (long long)c0 * IC * d, d, (long long)IC * d,
-                    dX + (long long)c0 * IC * d, d, (long long)IC * d, 0.0f, T, IC, (long long)IC * IC, r1 - c0, 0, 0,
-                    nullptr, 0);
+      if (rbf)
+        rc = sig_fo_mf_cells(dX, n1, l1, dX, n1, l1, d, pm, c0, r1, T, c0, 0, (long long)IC * IC, 0, IC, s);
+      else
+        rc = gemm_f32(s, false, true, IC, IC, d, 1.0f, dX + (long long)c0 * IC * d, d, (long long)IC * d,
+                      dX + (long long)c0 * IC * d, d, (long long)IC * d, 0.0f, T, IC, (long long)IC * IC, r1 - c0, 0, 0,
+                      nullptr, 0);
     } else {
       const int b0 = pm == GPSIG_PAIRS_UPPER ? r0 : 0;
       const long long tc = (long long)(n2 - b0) * JC;
@@ -394,9 +429,12 @@ int sig_ho_tiled(SigArgs a, const float *X, const float *Y, int d, void *workspa
         c.tile_base = ho_upper_prefix(ta0, n2);
         nblocks = ho_upper_prefix(ta1, n2) - c.tile_base;
       }
-      rc = gemm_f32(s, false, true, (r1 - r0) * IC, (int)tc, d, 1.0f, dX + (long long)r0 * IC * d, d, 0,
-                    dY + (long long)b0 * JC * d, d, 0, 0.0f, T, tc, 0, 1, pm == GPSIG_PAIRS_UPPER ? IC : 0,
-                    pm == GPSIG_PAIRS_UPPER ? JC : 0, nullptr, 0);
+      if (rbf)
+        rc = sig_fo_mf_cells(dX, n1, l1, dY, n2, l2, d, pm, c0, r1, T, r0, b0, (long long)IC * tc, JC, tc, s);
+      else
+        rc = gemm_f32(s, false, true, (r1 - r0) * IC, (int)tc, d, 1.0f, dX + (long long)r0 * IC * d, d, 0,
+                      dY + (long long)b0 * JC * d, d, 0, 0.0f, T, tc, 0, 1, pm == GPSIG_PAIRS_UPPER ? IC : 0,
+                      pm == GPSIG_PAIRS_UPPER ? JC : 0, nullptr, 0);
     }
     if (rc) return rc;
     if (nblocks > 0x7fffffffLL) return GPSIG_EUNSUPPORTED;

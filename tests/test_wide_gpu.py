@@ -292,13 +292,24 @@ def test_wide_higher_order_linear(D, L, M, order):
     assert (norm_rel_err(d[1:], np.stack([np.diagonal(e) for e in exp])[1:], axis_levels=True) < TOL).all()
 
 
-def test_wide_higher_order_rbf_raises():
-    """The tile mode builds linear cells only: the RBF higher-order recursion past 32 channels raises."""
-    from gpsig_amd import _lib as Lb
+@pytest.mark.parametrize("D,L,M,order", [(46, 40, 3, 2), (33, 100, 4, 3), (126, 60, 5, 5), (46, 170, 3, 2)])
+def test_wide_higher_order_rbf(D, L, M, order):
+    """Higher-order recursion past 32 channels with the RBF base kernel (signature_algs.py:37-74 over
+    kernels.py:946-957 at any D): the difference-seed cells of each chunk of pairs come from the matrix-core
+    wide seed in cell-producer mode (sig_fo_mf.h; column blocks at L = 170), the recursion reads them as the
+    linear path reads its increment Gram, level 1 in the RBF closed form.  Cross, symmetric and diagonal
+    against the fp64 oracle."""
     from gpsig_amd import ops
-    X = torch.zeros((2, 10, 40), device=DEV)
-    with pytest.raises(Lb.GpsigError):
-        ops.sig_gram(X, None, 3, order=2, base="rbf")
+    rng = np.random.default_rng(D + L + order + 1)
+    X, Y = walks(rng, 4, L, D), walks(rng, 3, L - 5, D)
+    ref = kr.SignatureKernelRef(L * D, D, M, normalization=False, order=order)
+    got = ops.sig_gram(t(X), t(Y), M, order=order, base="rbf").cpu().numpy()
+    assert (norm_rel_err(got[1:], ref.K_seq(X, Y)[1:], axis_levels=True) < TOL).all()
+    S = ops.sig_gram(t(X), None, M, order=order, base="rbf").cpu().numpy()
+    exp = ref.K_seq(X, X)
+    assert (norm_rel_err(S[1:], exp[1:], axis_levels=True) < TOL).all()
+    dg = ops.sig_diag(t(X), M, order=order, base="rbf").cpu().numpy()
+    assert (norm_rel_err(dg[1:], np.stack([np.diagonal(e) for e in exp])[1:], axis_levels=True) < TOL).all()
 
 
 # ----------------------------------------------------------------------------- edge cases
@@ -418,3 +429,21 @@ def test_wide_vjp_column_side_split_k():
     assert norm_rel_err(gy[sel], Yr.grad.numpy()) < GTOL
     rest = np.setdiff1d(np.arange(N2), sel)
     assert not np.any(gy[rest])
+
+
+@pytest.mark.parametrize("D,L,M,base", [(46, 161, 2, "rbf"), (46, 300, 6, "rbf"), (126, 300, 3, "rbf"),
+                                        (46, 300, 4, "linear"), (200, 170, 3, "rbf")])
+def test_wide_mf_column_blocks(D, L, M, base):
+    """Matrix-core wide Gram past 160 points (sig_fo_mf.h): column blocks of 127 cells, each with its own B
+    image (the block's increments and its first point y_{j0}), the levels' column sums carried from block to
+    block through the workspace; K(X, X2) at ragged lengths and K(X), raw levels against the oracle."""
+    from gpsig_amd import ops
+    rng = np.random.default_rng(D + L + M)
+    X = walks(rng, 5, L, D)
+    Y = walks(rng, 3, L - 11, D)
+    ref = kr.SignatureKernelRef(L * D, D, M, normalization=False, base=base)
+    got = ops.sig_gram(t(X), t(Y), M, base=base).cpu().numpy()
+    assert (norm_rel_err(got[1:], ref.K_seq(X, Y)[1:], axis_levels=True) < TOL).all()
+    sym = ops.sig_gram(t(X), None, M, base=base).cpu().numpy()
+    assert (norm_rel_err(sym[1:], ref.K_seq(X)[1:], axis_levels=True) < TOL).all()
+    np.testing.assert_array_equal(sym, np.swapaxes(sym, 1, 2))

@@ -4,7 +4,7 @@ device-synchronised calls, inputs resident), with the gradient's error vs torch 
 reference graph (oracle/autodiff_ref.py) / the reference's PDE adjoint (oracle/pde_grad.py) on a
 subsample.  One JSON object per line.
 
-    python tools/bench_grad.py [--only gram,kuf,kuf_incr,pde,pde_gram,sig]
+    python tools/bench_grad.py [--only gram,kuf,kuf_incr,pde,pde_gram,sig,svgp46,svgp126]
 """
 import argparse
 import json
@@ -180,6 +180,47 @@ def bench_sig(reps, n=4096, l=100, d=5, depth=3):
                 fwd_bwd_ms=tb * 1e3, grad_err=rel(Xg.grad[0].cpu().numpy(), xs.grad.numpy()))
 
 
+def bench_svgp(reps, t=500, n=50, l=500, nf=23, m=4):
+    """One SVGP training step's kernel bundle at the reference runner's shapes
+    (benchmarks/run_gpsig_benchmarks.py:32 -> models/train_gpsig.py:20-58): SignatureRBF(num_levels=4,
+    num_lags=1, add_time) with InducingTensors(num_inducing=500, increments=True), a minibatch of 50
+    sequences of max_len 500; nf raw features + time, so D = 2 nf after the lag (46 AUSLAN, 126 CMU).
+    Kuu_Kuf_Kff (inducing_variables.py:51-67) forward, then the backward to Z, the lengthscales and the
+    variances (X is data).  The gradient paths are parity-tested in tests/ (test_wide_gpu, test_training_gpu);
+    this row is timing only."""
+    import gpsig_amd
+    from gpsig_amd.inducing_variables import InducingTensors
+    D = 2 * nf
+    lt = m * (m + 1) // 2
+    rng = np.random.default_rng(5)
+    Xnp = walks(n, l, nf, 0)
+    X = torch.tensor(Xnp.reshape(n, -1), device="cuda", dtype=torch.float64)
+    Z0 = torch.tensor(rng.standard_normal((lt, t, 2, D)) * 0.3, device="cuda", dtype=torch.float64)
+    k = gpsig_amd.SignatureRBF(l * nf, nf, m, num_lags=1, lengthscales=np.ones(nf))
+    k.to("cuda")
+    Gzz = torch.randn(t, t, device="cuda", dtype=torch.float64)
+    Gzx = torch.randn(t, n, device="cuda", dtype=torch.float64)
+    Gxx = torch.randn(n, device="cuda", dtype=torch.float64)
+
+    def step(grad):
+        feat = InducingTensors(Z0.detach().requires_grad_(grad), m, increments=True)
+        if grad:
+            for v in (k.lengthscales, k.variances):
+                v.requires_grad_(True)
+                v.grad = None
+        with torch.set_grad_enabled(grad):
+            Kzz, Kzx, Kxx = feat.Kuu_Kuf_Kff(k, X, jitter=1e-6)
+            if grad:
+                ((Kzz * Gzz).sum() + (Kzx * Gzx).sum() + (Kxx * Gxx).sum()).backward()
+
+    tf, tb = timed(lambda: step(False), reps), timed(lambda: step(True), reps)
+    for v in (k.lengthscales, k.variances):
+        v.requires_grad_(False)
+    return dict(path=f"svgp_d{D}", workload=f"SVGP step Kuu_Kuf_Kff SignatureRBF num_levels={m} num_lags=1 D={D} "
+                f"InducingTensors T={t} increments=True, minibatch N={n} L={l} (dZ, dlengthscales, dvariances)",
+                fwd_ms=tf * 1e3, fwd_bwd_ms=tb * 1e3, grad_err=None)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
@@ -189,7 +230,8 @@ def main():
     runs = dict(gram=lambda: bench_gram(a.reps), kuf=lambda: bench_kuf(a.reps),
                 kuf_incr=lambda: bench_kuf(a.reps, increments=True), pde=lambda: bench_pde(a.reps),
                 pde_gram=lambda: bench_pde_gram(a.reps),
-                sig=lambda: bench_sig(a.reps))
+                sig=lambda: bench_sig(a.reps), svgp46=lambda: bench_svgp(a.reps, nf=23),
+                svgp126=lambda: bench_svgp(a.reps, nf=63))
     for name in todo:
         r = runs[name]()
         r["bwd_over_fwd"] = (r["fwd_bwd_ms"] - r["fwd_ms"]) / r["fwd_ms"]
