@@ -1,7 +1,7 @@
 // gpsig_amd -- launches of the higher-order Gram VJP kernel (sig_ho_bwd.h): orders 2 (levels 2..8) and 3
 // (levels 3..5), the (order, levels) whose multiplier slab fits the LDS next to the cell buffer.  Orders
 // at or above the level count are the exact signature kernel: order min(order, M).
-#include "sig_ho_bwd.h"
+#include "sig_ho_bwd_lds.h"
 
 namespace gpsig {
 
@@ -22,15 +22,44 @@ static int launch_ho_bwd(const BwdArgs &a, int seed, long long nblocks, hipStrea
 
 static int ho_eff_order(int order, int M) { return order < M ? order : M; }
 
+// the register kernel (sig_ho_bwd.h: one pair per wave, 4 per workgroup)
+static bool ho_bwd_reg(int l2, int o, int M) { return l2 <= 256 && (o == 2 || (o == 3 && M <= 5)); }
+
 bool ho_bwd_supported(int l2, int order, int M, int seed) {
   if (seed != SEED_RBF_DIFF && seed != SEED_LIN_DIFF) return false;
-  if (l2 < 2 || l2 > 256 || M < 2 || M > 8 || order < 2) return false;
+  if (l2 < 2 || l2 > 512 || M < 2 || M > 8 || order < 2) return false;
   const int o = ho_eff_order(order, M);
-  return o == 2 || (o == 3 && M <= 5);
+  return ho_bwd_reg(l2, o, M) || (o <= HO_LDS_MAX_ORD && ho_bwd_lds_fits(o, M, l2));
+}
+
+// The LDS kernel runs one pair per workgroup: its own grid over the launch's rows [row_begin, row_end)
+static int ho_bwd_lds_launch(BwdArgs a, int o, int seed, hipStream_t s) {
+  const int r0 = a.row_begin, r1 = a.row_end;
+  long long nblocks;
+  if (a.pair_mode == GPSIG_PAIRS_DIAG) {
+    nblocks = r1 - r0;
+  } else if (a.pair_mode == GPSIG_PAIRS_UPPER) {
+    auto P = [&](long long r) { return r * a.n2 - r * (r - 1) / 2; };
+    a.tile_base = P(r0);
+    nblocks = P(r1) - P(r0);
+  } else {
+    nblocks = (long long)(r1 - r0) * a.n2;
+  }
+  a.blk0 = 0;
+  if (nblocks <= 0) return GPSIG_OK;
+  if (nblocks > 0x7fffffffLL) return GPSIG_EUNSUPPORTED;
+  switch (o) {
+    case 2: return sig_ho_bwd_lds_launch_o<2>(a, seed, nblocks, s);
+    case 3: return sig_ho_bwd_lds_launch_o<3>(a, seed, nblocks, s);
+    case 4: return sig_ho_bwd_lds_launch_o<4>(a, seed, nblocks, s);
+    case 5: return sig_ho_bwd_lds_launch_o<5>(a, seed, nblocks, s);
+    default: return GPSIG_EUNSUPPORTED;
+  }
 }
 
 int sig_ho_bwd_launch(const BwdArgs &a, int order, int seed, long long nblocks, hipStream_t s) {
   const int o = ho_eff_order(order, a.M);
+  if (!ho_bwd_reg(a.l2, o, a.M)) return ho_bwd_lds_launch(a, o, seed, s);
   switch (o * 16 + a.M) {
     case 2 * 16 + 2: return launch_ho_bwd<2, 2>(a, seed, nblocks, s);
     case 2 * 16 + 3: return launch_ho_bwd<2, 3>(a, seed, nblocks, s);

@@ -75,11 +75,11 @@ def test_higher_order_diag_and_norms_gradient():
 
 
 def test_unsupported_higher_order_gradients_raise():
-    """Orders past the VJP kernel (min(order, num_levels) = 4 here) that are not the exact linear kernel
+    """Orders past the VJP kernels (min(order, num_levels) = 6 here) that are not the exact linear kernel
     evaluate forward; their backward raises."""
     import gpsig_amd
     X = torch.tensor(golden("linear_chen.npz")["X"][:4].reshape(4, -1), device=DEV, requires_grad=True)
-    for k in (gpsig_amd.SignatureRBF(60, 3, 5, order=4), gpsig_amd.SignatureLinear(60, 3, 5, order=4)):
+    for k in (gpsig_amd.SignatureRBF(60, 3, 6, order=6), gpsig_amd.SignatureLinear(60, 3, 7, order=6)):
         K = k.K(X)
         with pytest.raises(NotImplementedError):
             K.sum().backward()
@@ -92,11 +92,14 @@ def _walks(n, l, d, seed):
 @pytest.mark.parametrize("L,D,M,order,base", [
     (12, 3, 3, 2, "rbf"), (30, 4, 5, 2, "linear"), (40, 46, 4, 2, "rbf"), (200, 3, 4, 2, "rbf"),
     (25, 3, 4, 3, "rbf"), (20, 2, 5, 3, "linear"), (18, 3, 3, 3, "linear"), (16, 2, 8, 2, "rbf"),
+    # the LDS-state kernel (csrc/sig_ho_bwd_lds.h): orders 4-5, order 3 past 5 levels, 257-512 points
+    (25, 3, 5, 4, "rbf"), (20, 2, 5, 5, "linear"), (22, 3, 6, 3, "rbf"), (16, 2, 7, 5, "rbf"),
+    (19, 4, 4, 4, "linear"), (300, 3, 4, 2, "rbf"), (270, 2, 5, 5, "linear"), (400, 3, 5, 4, "rbf"),
 ])
 def test_higher_order_vjp_kernel_raw_levels(L, D, M, order, base):
-    """gpsig_sig_gram_vjp_ho (csrc/sig_ho_bwd.h) against fp64 autodiff of signature_kern_higher_order
-    (signature_algs.py:37-74, restated in oracle/autodiff_ref.py): per-level upstream gradients, cross
-    K(X, Y), symmetric K(X) (UPPER pairs) and the diagonal."""
+    """gpsig_sig_gram_vjp_ho (csrc/sig_ho_bwd.h, sig_ho_bwd_lds.h) against fp64 autodiff of
+    signature_kern_higher_order (signature_algs.py:37-74, restated in oracle/autodiff_ref.py): per-level
+    upstream gradients, cross K(X, Y), symmetric K(X) (UPPER pairs) and the diagonal."""
     from gpsig_amd import ops
     X, Y = _walks(3, L, D, L + order), _walks(4, L - 3, D, L + order + 1)
     G = np.random.default_rng(7).standard_normal((M + 1, 3, 4))
@@ -152,16 +155,75 @@ def test_higher_order_normalised_K_gradient(cross, base):
 
 
 def test_higher_order_vjp_unsupported_raises():
-    """min(order, M) = 4 and sequences past 256 points are outside the VJP kernel: the error names the
-    entry point (autograd then uses the signature-feature path for the exact linear kernel, or raises)."""
+    """min(order, M) = 6, sequences past 512 points, and (order, levels) whose multiplier slab does not fit
+    the LDS at 257-512 points are outside the VJP kernels: the error names the entry point (autograd then
+    uses the signature-feature path for the exact linear kernel, or raises)."""
     from gpsig_amd import _lib as Lb
     from gpsig_amd import ops
-    X = torch.zeros((2, 10, 2), device=DEV)
-    with pytest.raises(Lb.GpsigError):
-        ops.sig_gram_vjp(X, None, 5, torch.zeros((6, 2, 2), device=DEV), gout_levels=True, order=4)
-    X = torch.zeros((2, 300, 2), device=DEV)
-    with pytest.raises(Lb.GpsigError):
-        ops.sig_gram_vjp(X, None, 3, torch.zeros((4, 2, 2), device=DEV), gout_levels=True, order=2)
+    for L, M, order in ((10, 6, 6), (600, 3, 2), (300, 6, 4), (300, 8, 3)):
+        X = torch.zeros((2, L, 2), device=DEV)
+        with pytest.raises(Lb.GpsigError):
+            ops.sig_gram_vjp(X, None, M, torch.zeros((M + 1, 2, 2), device=DEV), gout_levels=True, order=order)
+
+
+@pytest.mark.parametrize("normalization", [True, False])
+def test_higher_order_long_sequences_gradient(normalization):
+    """SignatureLinear(num_levels=5, order=5) at the VOSF trainer's sequence shape (d = 24, L = 500,
+    benchmarks/models/train_gpsig_vosf.py:102): K (symmetric and cross) and Kdiag gradients through the
+    LDS-state VJP kernel (W = 8 columns per lane), vs fp64 autodiff of the reference graph."""
+    import gpsig_amd
+    from gpsig_amd import ops
+    N, L, D, M = 2, 500, 24, 5
+    assert ops.ho_vjp_supported(L, M, M, "linear")
+    X, X2 = _walks(N, L, D, 21), _walks(2, L - 20, D, 22)
+    k = gpsig_amd.SignatureLinear(L * D, D, M, order=M, normalization=normalization)
+    Xt = torch.tensor(X.reshape(N, -1), device=DEV, dtype=torch.float32, requires_grad=True)
+    X2t = torch.tensor(X2.reshape(2, -1), device=DEV, dtype=torch.float32, requires_grad=True)
+    G, G2 = np.random.default_rng(23).standard_normal((N, N)), np.random.default_rng(24).standard_normal((N, 2))
+    Gd = np.random.default_rng(25).standard_normal(N)
+    (k.K(Xt) * torch.as_tensor(G, device=DEV)).sum().backward()
+    gs = Xt.grad.reshape(X.shape).cpu().numpy()
+    Xt.grad = None
+    (k.K(Xt, X2t) * torch.as_tensor(G2, device=DEV)).sum().backward()
+    gc, gc2 = Xt.grad.reshape(X.shape).cpu().numpy(), X2t.grad.reshape(X2.shape).cpu().numpy()
+    if not normalization:  # the normalised diagonal is the constant sum of the variances
+        Xt.grad = None
+        (k.Kdiag(Xt) * torch.as_tensor(Gd, device=DEV)).sum().backward()
+        gd = Xt.grad.reshape(X.shape).cpu().numpy()
+
+    def ref(Y, Gm):
+        """fp64 gradients, and the scale the criterion is relative to: normalised, the gradient is the
+        small difference of the raw-level term and the diagonal terms (K_m is homogeneous of degree 2m in
+        the path, its normalisation scale-invariant), so the error is measured against the raw term alone
+        (the gradient with the normalising diagonals held fixed)"""
+        Xr = torch.tensor(X, requires_grad=True)
+        Yr = None if Y is None else torch.tensor(Y, requires_grad=True)
+        (ar.K(Xr, Yr, M, base="linear", normalization=normalization, order=M) * torch.tensor(Gm)).sum().backward()
+        out = [Xr.grad.numpy()] + ([] if Y is None else [Yr.grad.numpy()])
+        if not normalization:
+            return out, [np.linalg.norm(o) for o in out]
+        Xs = torch.tensor(X, requires_grad=True)
+        Ys = None if Y is None else torch.tensor(Y, requires_grad=True)
+        Kl = ar.k_seq(Xs, Ys, M, "linear", order=M)
+        if Y is None:
+            dd = torch.sqrt(torch.diagonal(Kl, dim1=1, dim2=2).detach() + 1e-6)
+            den = dd[:, :, None] * dd[:, None, :]
+        else:
+            d1 = torch.sqrt(ar.k_seq_diag(Xs.detach(), M, "linear", order=M) + 1e-6)
+            d2 = torch.sqrt(ar.k_seq_diag(Ys.detach(), M, "linear", order=M) + 1e-6)
+            den = d1[:, :, None] * d2[:, None, :]
+        ((Kl / den).sum(0) * torch.tensor(Gm)).sum().backward()
+        return out, [np.linalg.norm(Xs.grad.numpy())] + ([] if Y is None else [np.linalg.norm(Ys.grad.numpy())])
+
+    (rs,), (ns,) = ref(None, G)
+    assert np.linalg.norm(gs - rs) < GTOL * ns
+    (rc, rc2), (nc, nc2) = ref(X2, G2)
+    assert np.linalg.norm(gc - rc) < GTOL * nc
+    assert np.linalg.norm(gc2 - rc2) < GTOL * nc2
+    if not normalization:
+        Xr = torch.tensor(X, requires_grad=True)
+        (ar.k_seq_diag(Xr, M, "linear", True, order=M).sum(0) * torch.tensor(Gd)).sum().backward()
+        assert norm_rel_err(gd, Xr.grad.numpy()) < GTOL
 
 
 @pytest.mark.parametrize("L1,L2,D", [(2, 2, 3), (3, 40, 2), (2, 9, 40)])
