@@ -80,7 +80,8 @@ SIGNATURES = {
     "gpsig_tens_vs_seq_state": (_I, [_P, _I, _I, _I, _I, _P, _I, _I, _I, _I, _P, _P, _P, _SZ, _P]),
     "gpsig_tens_vjp_workspace_bytes": (_SZ, [_I, _I, _I]),
     "gpsig_tens_vjp_wide_workspace_bytes": (_SZ, [_I, _I, _I, _I, _I]),
-    "gpsig_tens_gram_vjp": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P]),
+    "gpsig_tens_gram_vjp_workspace_bytes": (_SZ, [_I, _I, _I, _I, _I, _I]),
+    "gpsig_tens_gram_vjp": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P, _P, _SZ, _P]),
     "gpsig_rescaled": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _P, _P, _SZ, _P]),
     "gpsig_rescaled_workspace_bytes": (_SZ, [_I, _I]),
     "gpsig_tens_workspace_bytes": (_SZ, [_I, _I, _I, _I, _I]),

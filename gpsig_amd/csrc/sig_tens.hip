@@ -790,24 +790,19 @@ struct TgBwdArgs {
   int t, d, incr, rbf, chunk;
   const float *gout;  // (M+1, T, T)
   float *gZ;          // like Z, accumulated
-  int q0;             // WIDE: this launch accumulates the channels q0 .. q0 + DP - 1 of the gradient
 };
 
-// WIDE: the component values m_c are products over all d channels (runtime loops), the gradient
-// accumulators cover one window of DP channels (the host launches one window after the other).
-template <int DP, bool WIDE = false>
+// Channel counts up to 32 (DP = 4 .. 32, padded channels read as zeros); wider ones: tens_vjp_mm.hip.
+template <int DP>
 __global__ __launch_bounds__(64) void tens_gram_vjp_kernel(TgBwdArgs a) {
   const int t1 = blockIdx.x * 64 + threadIdx.x;
   if (t1 >= a.t) return;
   const int i = blockIdx.y + 1, k0 = i * (i - 1) / 2;
   const int tb = blockIdx.z * a.chunk, te = min(a.t, tb + a.chunk);
   const int d = a.d, T = a.t, zs = a.incr ? 2 * d : d;
-  const int q0 = WIDE ? a.q0 : 0;
   auto zv = [&](int k, int tt, int h, int q) -> float {
     return q < d ? a.Z[((long long)k * T + tt) * zs + h * d + q] : 0.f;
   };
-  // the accumulated window: channel q0 + q
-  auto zw = [&](int k, int tt, int h, int q) -> float { return zv(k, tt, h, q0 + q); };
   float g0[TV_MMAX][DP], g1[TV_MMAX][DP];
 #pragma unroll
   for (int c = 0; c < TV_MMAX; ++c)
@@ -820,25 +815,7 @@ __global__ __launch_bounds__(64) void tens_gram_vjp_kernel(TgBwdArgs a) {
     for (int c = 0; c < TV_MMAX; ++c) {
       if (c >= i) break;
       const int k = k0 + c;
-      if constexpr (WIDE) {
-        if (!a.incr) {
-          float s2 = 0.f, ip = 0.f;
-          for (int q = 0; q < d; ++q) {
-            const float df = zv(k, t1, 0, q) - zv(k, t2, 0, q);
-            s2 = __builtin_fmaf(df, df, s2);
-            ip = __builtin_fmaf(zv(k, t1, 0, q), zv(k, t2, 0, q), ip);
-          }
-          m[c] = a.rbf ? fast_exp(-0.5f * s2) : ip;
-        } else if (a.rbf) {
-          m[c] = rbf_second_diff_rt(
-              d, [&](int q) { return zv(k, t1, 0, q); }, [&](int q) { return zv(k, t1, 1, q) - zv(k, t1, 0, q); },
-              [&](int q) { return zv(k, t2, 0, q); }, [&](int q) { return zv(k, t2, 1, q) - zv(k, t2, 0, q); });
-        } else {
-          float v = 0.f;
-          for (int q = 0; q < d; ++q) v = __builtin_fmaf(zv(k, t1, 1, q) - zv(k, t1, 0, q), zv(k, t2, 1, q) - zv(k, t2, 0, q), v);
-          m[c] = v;
-        }
-      } else if (!a.incr) {
+      if (!a.incr) {
         float s2 = 0.f, ip = 0.f;
 #pragma unroll
         for (int q = 0; q < DP; ++q) {
@@ -877,7 +854,7 @@ __global__ __launch_bounds__(64) void tens_gram_vjp_kernel(TgBwdArgs a) {
       const float w = Gs * pre[c] * suf;
       suf *= m[c];
       const int k = k0 + c;
-      const int nq = WIDE ? d : DP;  // channels of the distances (all of them)
+      constexpr int nq = DP;
       if (!a.incr) {
         if (a.rbf) {
           float s2 = 0.f;
@@ -888,10 +865,10 @@ __global__ __launch_bounds__(64) void tens_gram_vjp_kernel(TgBwdArgs a) {
           }
           const float wk = w * fast_exp(-0.5f * s2);
 #pragma unroll
-          for (int q = 0; q < DP; ++q) g0[c][q] = __builtin_fmaf(wk, zw(k, t2, 0, q) - zw(k, t1, 0, q), g0[c][q]);
+          for (int q = 0; q < DP; ++q) g0[c][q] = __builtin_fmaf(wk, zv(k, t2, 0, q) - zv(k, t1, 0, q), g0[c][q]);
         } else {
 #pragma unroll
-          for (int q = 0; q < DP; ++q) g0[c][q] = __builtin_fmaf(w, zw(k, t2, 0, q), g0[c][q]);
+          for (int q = 0; q < DP; ++q) g0[c][q] = __builtin_fmaf(w, zv(k, t2, 0, q), g0[c][q]);
         }
       } else if (a.rbf) {
         // dM/dA1 = k(A1,B1)(B1 - A1) - k(A1,B0)(B0 - A1),  dM/dA0 = k(A0,B0)(B0 - A0) - k(A0,B1)(B1 - A0)
@@ -908,14 +885,14 @@ __global__ __launch_bounds__(64) void tens_gram_vjp_kernel(TgBwdArgs a) {
         const float k00 = w * fast_exp(-0.5f * e00), k01 = w * fast_exp(-0.5f * e01);
 #pragma unroll
         for (int q = 0; q < DP; ++q) {
-          const float a0 = zw(k, t1, 0, q), a1 = zw(k, t1, 1, q), b0 = zw(k, t2, 0, q), b1 = zw(k, t2, 1, q);
+          const float a0 = zv(k, t1, 0, q), a1 = zv(k, t1, 1, q), b0 = zv(k, t2, 0, q), b1 = zv(k, t2, 1, q);
           g1[c][q] += k11 * (b1 - a1) - k10 * (b0 - a1);
           g0[c][q] += k00 * (b0 - a0) - k01 * (b1 - a0);
         }
       } else {
 #pragma unroll
         for (int q = 0; q < DP; ++q) {
-          const float dBq = zw(k, t2, 1, q) - zw(k, t2, 0, q);
+          const float dBq = zv(k, t2, 1, q) - zv(k, t2, 0, q);
           g1[c][q] = __builtin_fmaf(w, dBq, g1[c][q]);
           g0[c][q] = __builtin_fmaf(-w, dBq, g0[c][q]);
         }
@@ -925,10 +902,10 @@ __global__ __launch_bounds__(64) void tens_gram_vjp_kernel(TgBwdArgs a) {
 #pragma unroll
   for (int c = 0; c < TV_MMAX; ++c) {
     if (c >= i) break;
-    float *gz = a.gZ + ((long long)(k0 + c) * T + t1) * zs + q0;
+    float *gz = a.gZ + ((long long)(k0 + c) * T + t1) * zs;
 #pragma unroll
     for (int q = 0; q < DP; ++q) {
-      if (q0 + q < d) {
+      if (q < d) {
         unsafeAtomicAdd(gz + q, g0[c][q]);
         if (a.incr) unsafeAtomicAdd(gz + d + q, g1[c][q]);
       }
@@ -988,28 +965,40 @@ extern "C" int gpsig_rescaled(const float *Z, int lt, int t, const float *X, int
   return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
 }
 
+namespace gpsig {
+size_t tens_gram_vjp_mm_bytes(int lt, int t, int incr, int d, int rbf);
+int tens_gram_vjp_mm(const float *Z, int lt, int t, int incr, int d, int M, int rbf, const float *gout, float *gZ,
+                     void *workspace, size_t workspace_bytes, hipStream_t s);
+}  // namespace gpsig
+
+// Channel counts past 32 take the pair-tile + GEMM path (tens_vjp_mm.hip), which needs a workspace.
+extern "C" size_t gpsig_tens_gram_vjp_workspace_bytes(int lt, int t, int increments, int d, int num_levels,
+                                                      int base_kind) {
+  if (lt <= 0 || t <= 0 || d <= 0 || num_levels < 1 || dpad4(d) != 0) return 0;
+  return gpsig::tens_gram_vjp_mm_bytes(lt, t, increments ? 1 : 0, d, base_kind == GPSIG_BASE_RBF ? 1 : 0);
+}
+
 extern "C" int gpsig_tens_gram_vjp(const float *Z, int lt, int t, int increments, int d, int num_levels,
-                                   int base_kind, const float *gout, float *gZ, gpsig_stream_t stream) {
+                                   int base_kind, const float *gout, float *gZ, void *workspace,
+                                   size_t workspace_bytes, gpsig_stream_t stream) {
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (!Z || !gout || !gZ || lt <= 0 || t <= 0 || d <= 0 || num_levels < 1) return GPSIG_EINVAL;
   if (lt != num_levels * (num_levels + 1) / 2) return GPSIG_EINVAL;
   if (num_levels > TV_MMAX) return GPSIG_EUNSUPPORTED;
   if (base_kind != GPSIG_BASE_RBF && base_kind != GPSIG_BASE_LINEAR) return GPSIG_EUNSUPPORTED;
   const int DP = dpad4(d);
+  if (DP == 0)
+    return gpsig::tens_gram_vjp_mm(Z, lt, t, increments ? 1 : 0, d, num_levels, base_kind == GPSIG_BASE_RBF ? 1 : 0, gout,
+                            gZ, workspace, workspace_bytes, s);
   const int chunk = 64;
-  TgBwdArgs a{Z, t, d, increments, base_kind == GPSIG_BASE_RBF, chunk, gout, gZ, 0};
+  TgBwdArgs a{Z, t, d, increments, base_kind == GPSIG_BASE_RBF, chunk, gout, gZ};
   dim3 grid((t + 63) / 64, num_levels, (t + chunk - 1) / chunk);
   switch (DP) {
     case 4: hipLaunchKernelGGL(tens_gram_vjp_kernel<4>, grid, dim3(64), 0, s, a); break;
     case 8: hipLaunchKernelGGL(tens_gram_vjp_kernel<8>, grid, dim3(64), 0, s, a); break;
     case 16: hipLaunchKernelGGL(tens_gram_vjp_kernel<16>, grid, dim3(64), 0, s, a); break;
     case 32: hipLaunchKernelGGL(tens_gram_vjp_kernel<32>, grid, dim3(64), 0, s, a); break;
-    default:  // wide: windows of 16 gradient channels, the component products over all d
-      for (int q0 = 0; q0 < d; q0 += 16) {
-        a.q0 = q0;
-        hipLaunchKernelGGL((tens_gram_vjp_kernel<16, true>), grid, dim3(64), 0, s, a);
-      }
-      break;
+    default: return GPSIG_EUNSUPPORTED;
   }
   return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
 }

@@ -628,8 +628,10 @@ def tens_gram_vjp(Z: torch.Tensor, num_levels: int, gout: torch.Tensor, base="rb
     gout = _f32(gout)
     if gZ is None:
         gZ = torch.zeros(Z.shape, dtype=torch.float32, device=Z.device)
+    nb = lib.gpsig_tens_gram_vjp_workspace_bytes(lt, t, int(increments), d, num_levels, base_kind(base))
+    ws = workspace(Z.device, nb) if nb else None
     rc = lib.gpsig_tens_gram_vjp(Z.data_ptr(), lt, t, int(increments), d, num_levels, base_kind(base), gout.data_ptr(),
-                                 gZ.data_ptr(), _stream(Z.device))
+                                 gZ.data_ptr(), _ptr(ws), ws.numel() if nb else 0, _stream(Z.device))
     L.check(rc, "gpsig_tens_gram_vjp")
     return gZ
 

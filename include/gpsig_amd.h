@@ -193,9 +193,12 @@ int gpsig_tens_gram(const float *Z, int lt, int t, int increments, int d, int nu
                     gpsig_stream_t stream);
 
 /* Gradient of gpsig_tens_gram (tensor_kern, signature_algs.py:76-99, over _K_tens, kernels.py:264-284):
- * gout (num_levels+1, T, T) = dLoss/d(raw per-level output); accumulates (+=) gZ (same layout as Z). */
+ * gout (num_levels+1, T, T) = dLoss/d(raw per-level output); accumulates (+=) gZ (same layout as Z).
+ * Channel counts past 32 run as pair tiles + matrix-core GEMMs and need the workspace the query names
+ * (0 for d <= 32: workspace may be NULL). */
+size_t gpsig_tens_gram_vjp_workspace_bytes(int lt, int t, int increments, int d, int num_levels, int base_kind);
 int gpsig_tens_gram_vjp(const float *Z, int lt, int t, int increments, int d, int num_levels, int base_kind,
-                        const float *gout, float *gZ, gpsig_stream_t stream);
+                        const float *gout, float *gZ, void *workspace, size_t workspace_bytes, gpsig_stream_t stream);
 
 /* gpsig_tens_vs_seq for a training step: the same output (order 1, difference 1, RBF or linear, d <= 8,
  * num_levels <= 6 -- the packed fast paths; GPSIG_EUNSUPPORTED otherwise, nothing launched) plus the

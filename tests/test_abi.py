@@ -79,7 +79,11 @@ def test_vjp_and_feature_entry_points_validate_arguments():
                                      None) == L.GPSIG_EINVAL
     assert lib.gpsig_tens_vs_seq_state(None, 6, 2, 0, 3, None, 4, 10, 3, 0, None, None, None, 0,
                                        None) == L.GPSIG_EINVAL
-    assert lib.gpsig_tens_gram_vjp(None, 6, 2, 0, 3, 3, 0, None, None, None) == L.GPSIG_EINVAL
+    assert lib.gpsig_tens_gram_vjp(None, 6, 2, 0, 3, 3, 0, None, None, None, 0, None) == L.GPSIG_EINVAL
+    # the pair-tile + GEMM path past 32 channels: m (LT T^2), kv (4 LT T^2), [Z_h | 1] and G (LT 2 T (d + 1))
+    assert lib.gpsig_tens_gram_vjp_workspace_bytes(10, 64, 1, 3, 4, L.BASE_RBF) == 0
+    assert lib.gpsig_tens_gram_vjp_workspace_bytes(10, 64, 1, 46, 4, L.BASE_RBF) == \
+        (10 * 64 * 64 + 40 * 64 * 64 + 2 * 20 * 64 * 47) * 4
     assert lib.gpsig_pde_vjp(None, 4, 10, None, 4, 10, 3, 0, 1, 0, 0, 4, None, None, None, None, 0,
                              None) == L.GPSIG_EINVAL
     assert lib.gpsig_signature(None, 4, 10, 3, 3, None, None) == L.GPSIG_EINVAL

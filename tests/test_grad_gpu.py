@@ -326,15 +326,17 @@ def test_tens_vs_seq_vjp_matches_autodiff(base, increments, M, D, L):
 
 @pytest.mark.parametrize("base", ["rbf", "linear"])
 @pytest.mark.parametrize("increments", [False, True])
-def test_tens_gram_vjp_matches_autodiff(base, increments):
-    """K_tens (Kzz, summed over levels x sigma*variances) gradients in Z and lengthscales."""
+@pytest.mark.parametrize("D", [3, 46])
+def test_tens_gram_vjp_matches_autodiff(base, increments, D):
+    """K_tens (Kzz, summed over levels x sigma*variances) gradients in Z and lengthscales (D = 46: the
+    pair-tile + GEMM path, csrc/tens_vjp_mm.hip)."""
     import gpsig_amd
-    M, T, D = 4, 70, 3
+    M, T = 4, 70
     LT = M * (M + 1) // 2
     rng = np.random.default_rng(30)
-    Z = 0.5 * rng.standard_normal((LT, T, 2, D) if increments else (LT, T, D))
+    Z = (0.5 if D <= 8 else 0.15) * rng.standard_normal((LT, T, 2, D) if increments else (LT, T, D))
     G = rng.standard_normal((T, T))
-    ls = np.array([0.9, 1.1, 1.3])
+    ls = np.linspace(0.9, 1.3, D)
     cls = gpsig_amd.SignatureRBF if base == "rbf" else gpsig_amd.SignatureLinear
     k = cls(10 * D, D, M)
     k.lengthscales = torch.tensor(ls, device=DEV, requires_grad=True)
