@@ -675,9 +675,10 @@ static int dpad4(int d) { return d <= 4 ? 4 : d <= 8 ? 8 : d <= 16 ? 16 : d <= 3
 namespace gpsig {
 int tvs_pk_launch(const float *Z, int lt, int t, int increments, int d, const float *Ft, int n, int l, int M,
                   float *out, float *Zp, bool rbf, float *state, hipStream_t s);
-int tvs_wide_launch(const float *Z, int lt, int t, int increments, int d, const float *Ft, int n, int l, int M,
-                    float *out, float *Zw, bool rbf, float *state, hipStream_t s);
+int tvs_wide_launch(const float *Z, int lt, int t, int increments, int d, const float *X, const float *Ft, int n,
+                    int l, int M, float *out, float *Zw, bool rbf, float *state, void *seedws, hipStream_t s);
 size_t tvs_pk_zp_bytes(int lt, int t, int d);
+size_t tvs_seed_bytes(int n, int l, int d, int lt, int t);
 }  // namespace gpsig
 
 static size_t tvs_ft_bytes(int n, int l, int d) {
@@ -694,8 +695,12 @@ int tvs_features_launch(const float *X, int n, int l, int d, float *Ft, hipStrea
 }
 }  // namespace gpsig
 
+// features, prepared components, and (d > 8) the wide path's seed GEMM tile
 extern "C" size_t gpsig_tens_workspace_bytes(int n, int l, int d, int lt, int t) {
-  return tvs_ft_bytes(n, l, d) + tvs_pk_zp_bytes(lt, t, d);
+  return tvs_ft_bytes(n, l, d) + tvs_pk_zp_bytes(lt, t, d) + tvs_seed_bytes(n, l, d, lt, t);
+}
+static void *tvs_seed_ws(void *workspace, int n, int l, int d, int lt, int t) {
+  return static_cast<char *>(workspace) + tvs_ft_bytes(n, l, d) + tvs_pk_zp_bytes(lt, t, d);
 }
 
 extern "C" int gpsig_tens_vs_seq(const float *Z, int lt, int t, int increments, int d, const float *X, int n, int l,
@@ -718,8 +723,8 @@ extern "C" int gpsig_tens_vs_seq(const float *Z, int lt, int t, int increments, 
     int rc = tvs_pk_launch(Z, lt, t, increments, d, Ft, n, l, num_levels, out, Zp, base_kind == GPSIG_BASE_RBF,
                            nullptr, s);
     if (rc == -1 && d > 8)
-      rc = tvs_wide_launch(Z, lt, t, increments, d, Ft, n, l, num_levels, out, Zp, base_kind == GPSIG_BASE_RBF,
-                           nullptr, s);
+      rc = tvs_wide_launch(Z, lt, t, increments, d, X, Ft, n, l, num_levels, out, Zp, base_kind == GPSIG_BASE_RBF,
+                           nullptr, tvs_seed_ws(workspace, n, l, d, lt, t), s);
     if (rc != -1) return rc;
   }
   TvsArgs a{Z, Ft, lt, t, n, l, d, num_levels, order, increments, difference, base_kind == GPSIG_BASE_RBF, out};
@@ -756,7 +761,8 @@ extern "C" int gpsig_tens_vs_seq_state(const float *Z, int lt, int t, int increm
   float *Zp = reinterpret_cast<float *>(static_cast<char *>(workspace) + tvs_ft_bytes(n, l, d));
   int rc = tvs_pk_launch(Z, lt, t, increments, d, Ft, n, l, num_levels, out, Zp, base_kind == GPSIG_BASE_RBF, state, s);
   if (rc == -1 && d > 8)
-    rc = tvs_wide_launch(Z, lt, t, increments, d, Ft, n, l, num_levels, out, Zp, base_kind == GPSIG_BASE_RBF, state, s);
+    rc = tvs_wide_launch(Z, lt, t, increments, d, X, Ft, n, l, num_levels, out, Zp, base_kind == GPSIG_BASE_RBF, state,
+                         tvs_seed_ws(workspace, n, l, d, lt, t), s);
   return rc == -1 ? GPSIG_EUNSUPPORTED : rc;
 }
 

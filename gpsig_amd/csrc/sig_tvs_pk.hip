@@ -13,6 +13,7 @@
 // k (and Ep) are re-evaluated exactly every ANCHOR (32) cells.  Arguments past the polynomial range take
 // expm1 = e^x - 1 (a wave-uniform branch); with increments, |q| or |c| >= 2 (far-apart corners) takes
 // the plain corner difference of directly evaluated base-kernel values.
+#include "gemm.h"
 #include "sig_common.h"
 
 namespace gpsig {
@@ -316,18 +317,82 @@ __global__ __launch_bounds__(64) void tvs_lin_kernel(TvsPkArgs a) {
 }
 
 // ------------------------------------------------------------------------------------ wide channels
-// The same recursion and seeds (tvs_pk_kernel, tvs_lin_kernel) for any channel count: the per-step dots
-// <z_k, dx_s> (and <dz_k, dx_s>) of all LT components come from one runtime channel loop -- the lane's
-// dx_s[q] is loaded once per channel (coalesced, time-major features) and the wave-uniform component
-// values of that channel are scalar loads from the prepared [tensor][channel][component] buffer, so
-// nothing grows with d except the loop count.  One sequence per lane.
+// The same recursion and seeds (tvs_pk_kernel, tvs_lin_kernel) for any channel count.  The per-step dots
+// <z_k, dx_s> (and <dz_k, dx_s>) of all LT components, every tensor and every step of a chunk of sequences
+// are ONE matrix-core GEMM (gemm.hip) into a seed tile
+//     S[(t LT + k) H + h][s nc + j] = <w_{t,k,h}, dx_{n0 + j, s}>,   w = z0 | dz (RBF, increments; H = 2),
+//                                                                    z (RBF) or the linear seed's z / dz
+// which the recursion kernel streams (coalesced across its lanes = sequences, next step prefetched).  The
+// exact base-kernel values at the anchors (every ANCHOR cells) and the far-apart corners keep the runtime
+// channel loop over the prepared [tensor][channel][component] buffer.  One sequence per lane.
 struct TvsWideArgs {
   const float *Zw;  // (T, [2,] d, LT) then (T, LT) |dz|^2 / 2: tvs_wide_prep_kernel
   const float *Ft;  // time-major features (sig_tens.hip)
   int t, n, l, d;
   float *out;
   float *state;
+  const float *S;   // seed tile of the chunk [n0, n0 + nc): rows (t LT + k) H + h, row length sld
+  long long sld;
+  int n0, nc;
 };
+
+// seed-tile budget of one chunk of sequences
+constexpr size_t TVS_SEED_TILE_BYTES = (size_t)1 << 30;
+
+struct TvsSeedPlan {
+  int nc;
+  size_t a, dx, s;
+};
+
+inline TvsSeedPlan tvs_seed_plan(int n, int l, int d, int lt, int t) {
+  TvsSeedPlan p{};
+  const size_t per_seq = (size_t)(l - 1) * t * lt * 2 * sizeof(float);  // H = 2: the largest tile
+  long long nc = per_seq ? (long long)(TVS_SEED_TILE_BYTES / per_seq) : n;
+  nc = nc < 64 ? 64 : (nc / 64) * 64;
+  if (nc > ((n + 63) / 64) * 64) nc = ((n + 63) / 64) * 64;
+  p.nc = (int)nc;
+  p.a = (((size_t)t * lt * 2 * d * sizeof(float)) + 255) & ~(size_t)255;
+  p.dx = (((size_t)nc * (l - 1) * d * sizeof(float)) + 255) & ~(size_t)255;
+  p.s = (((size_t)nc * (l - 1) * t * lt * 2 * sizeof(float)) + 255) & ~(size_t)255;
+  return p;
+}
+
+// workspace of the wide path's GEMM seeds (0: d <= 8 runs the packed kernels)
+size_t tvs_seed_bytes(int n, int l, int d, int lt, int t) {
+  if (d <= 8 || l < 2) return 0;
+  const TvsSeedPlan p = tvs_seed_plan(n, l, d, lt, t);
+  return p.a + p.dx + p.s;
+}
+
+// A[(t LT + k) H + h][q]: the GEMM's component rows
+__global__ __launch_bounds__(256) void tvs_seed_a_kernel(const float *__restrict__ Z, int lt, int t, int d, int incr,
+                                                         int H, int lin, float *__restrict__ A) {
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long long)t * lt * H * d) return;
+  const int q = (int)(idx % d);
+  long long r = idx / d;
+  const int h = (int)(r % H);
+  r /= H;
+  const int k = (int)(r % lt), tt = (int)(r / lt);
+  const float *z = Z + ((long long)k * t + tt) * (incr ? 2 * d : d);
+  float v;
+  if (!incr) v = z[q];
+  else if (lin || h == 1) v = z[d + q] - z[q];  // the linear seed's w = z1 - z0, or dz
+  else v = z[q];
+  A[idx] = v;
+}
+
+// DX[(s nc + j)][q] = x_{n0 + j, s + 1, q} - x_{n0 + j, s, q}
+__global__ __launch_bounds__(256) void tvs_seed_dx_kernel(const float *__restrict__ X, int l, int d, int n0, int nc,
+                                                          float *__restrict__ DX) {
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long long)(l - 1) * nc * d) return;
+  const int q = (int)(idx % d);
+  const long long r = idx / d;
+  const int j = (int)(r % nc), s = (int)(r / nc);
+  const float *x = X + ((long long)(n0 + j) * l + s) * d + q;
+  DX[idx] = x[d] - x[0];
+}
 
 __host__ __device__ inline long long tvs_wide_zs(int d, int lt, bool incr) { return (long long)(incr ? 2 * d + 1 : d) * lt; }
 
@@ -360,11 +425,14 @@ __global__ __launch_bounds__(64) void tvs_wide_kernel(TvsWideArgs a) {
   constexpr float TVS_CORNER = 2.0f;
   constexpr float NHL2E = -0.72134752044448170f, L2E = 1.4426950408889634f;
   constexpr int ANCHOR = GPSIG_TVS_ANCHOR;
+  constexpr int H = (RBF && INCR) ? 2 : 1;
   const int lane = threadIdx.x;
   const int tt = blockIdx.y;
   const int n = a.n, d = a.d, FC = 2 * d + 3;
-  const int s0 = blockIdx.x * 64 + lane;
-  const int c0 = s0 < n ? s0 : n - 1;
+  const int sl0 = blockIdx.x * 64 + lane;  // sequence within the chunk
+  const int sl = sl0 < a.nc ? sl0 : a.nc - 1;
+  const int s0 = a.n0 + sl0;
+  const int c0 = a.n0 + sl;
   cfloat *z0 = as_const(a.Zw) + (long long)tt * tvs_wide_zs(d, LT, INCR);  // [q][k]
   cfloat *dz = z0 + (long long)d * LT;
   cfloat *hdz = z0 + (long long)2 * d * LT;
@@ -402,25 +470,28 @@ __global__ __launch_bounds__(64) void tvs_wide_kernel(TvsWideArgs a) {
   if constexpr (RBF) exact_all(0, kc, Ep);
 
   const int ncell = a.l - 1;
+  // the step's dots from the seed tile; the next step's are in flight while this one is processed
+  const float *srow = a.S + (long long)tt * LT * H * a.sld + sl;
+  auto seeds = [&](int s, float (&sq)[LT], float (&sc)[LT]) {
+#pragma unroll
+    for (int k = 0; k < LT; ++k) {
+      sq[k] = srow[(long long)(k * H) * a.sld + (long long)s * a.nc];
+      if constexpr (H == 2) sc[k] = srow[(long long)(k * H + 1) * a.sld + (long long)s * a.nc];
+      else sc[k] = 0.f;
+    }
+  };
+  float sq[LT], sc[LT];
+  seeds(0, sq, sc);
   for (int s = 0; s < ncell; ++s) {
-    float qv[LT], cv[LT];
+    float qv[LT], cv[LT], nq[LT], ncv[LT];
+    if (s + 1 < ncell) seeds(s + 1, nq, ncv);
     const float g = RBF ? ft(s, 2 * d + 1) : 0.f;
 #pragma unroll
     for (int k = 0; k < LT; ++k) {
-      qv[k] = -g;
-      cv[k] = 0.f;
-    }
-    for (int q = 0; q < d; ++q) {
-      const float dxv = ft(s, d + q);
-#pragma unroll
-      for (int k = 0; k < LT; ++k) {
-        if constexpr (RBF) {
-          qv[k] = __builtin_fmaf(z0[(long long)q * LT + k], dxv, qv[k]);
-          if constexpr (INCR) cv[k] = __builtin_fmaf(dz[(long long)q * LT + k], dxv, cv[k]);
-        } else {  // linear: the seed is <w_k, dx_s>, w = z or z1 - z0
-          qv[k] = __builtin_fmaf(INCR ? dz[(long long)q * LT + k] : z0[(long long)q * LT + k], dxv, qv[k]);
-        }
-      }
+      qv[k] = sq[k] - g;
+      cv[k] = sc[k];
+      sq[k] = nq[k];
+      sc[k] = ncv[k];
     }
     float m[LT];
     if constexpr (!RBF) {
@@ -518,12 +589,8 @@ __global__ __launch_bounds__(64) void tvs_wide_kernel(TvsWideArgs a) {
 }
 
 template <int M>
-static int launch_tvs_wide(const float *Z, int lt, int t, int incr, int d, const float *Ft, int n, int l, float *out,
-                           float *Zw, bool rbf, float *state, hipStream_t s) {
-  hipLaunchKernelGGL(tvs_wide_prep_kernel, dim3((unsigned)(((long long)lt * t + 255) / 256)), dim3(256), 0, s, Z, lt, t,
-                     d, incr, Zw);
-  TvsWideArgs a{Zw, Ft, t, n, l, d, out, state};
-  dim3 grid((unsigned)((n + 63) / 64), (unsigned)t);
+static int launch_tvs_wide(const TvsWideArgs &a, int incr, bool rbf, hipStream_t s) {
+  dim3 grid((unsigned)((a.nc + 63) / 64), (unsigned)a.t);
   if (rbf) {
     if (incr) hipLaunchKernelGGL((tvs_wide_kernel<M, true, true>), grid, dim3(64), 0, s, a);
     else hipLaunchKernelGGL((tvs_wide_kernel<M, false, true>), grid, dim3(64), 0, s, a);
@@ -534,20 +601,44 @@ static int launch_tvs_wide(const float *Z, int lt, int t, int incr, int d, const
   return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
 }
 
-int tvs_wide_launch(const float *Z, int lt, int t, int increments, int d, const float *Ft, int n, int l, int M,
-                    float *out, float *Zw, bool rbf, float *state, hipStream_t s) {
-  if (l < 2) return -1;
-  switch (M) {
-    case 1: return launch_tvs_wide<1>(Z, lt, t, increments, d, Ft, n, l, out, Zw, rbf, state, s);
-    case 2: return launch_tvs_wide<2>(Z, lt, t, increments, d, Ft, n, l, out, Zw, rbf, state, s);
-    case 3: return launch_tvs_wide<3>(Z, lt, t, increments, d, Ft, n, l, out, Zw, rbf, state, s);
-    case 4: return launch_tvs_wide<4>(Z, lt, t, increments, d, Ft, n, l, out, Zw, rbf, state, s);
-    case 5: return launch_tvs_wide<5>(Z, lt, t, increments, d, Ft, n, l, out, Zw, rbf, state, s);
-    case 6: return launch_tvs_wide<6>(Z, lt, t, increments, d, Ft, n, l, out, Zw, rbf, state, s);
-    case 7: return launch_tvs_wide<7>(Z, lt, t, increments, d, Ft, n, l, out, Zw, rbf, state, s);
-    case 8: return launch_tvs_wide<8>(Z, lt, t, increments, d, Ft, n, l, out, Zw, rbf, state, s);
-    default: return -1;
+// X: the raw (n, l, d) sequences (the seed GEMM's increments); seedws: tvs_seed_bytes(n, l, d, lt, t)
+int tvs_wide_launch(const float *Z, int lt, int t, int increments, int d, const float *X, const float *Ft, int n,
+                    int l, int M, float *out, float *Zw, bool rbf, float *state, void *seedws, hipStream_t s) {
+  if (l < 2 || M < 1 || M > 8 || !seedws) return -1;
+  const TvsSeedPlan pl = tvs_seed_plan(n, l, d, lt, t);
+  char *w = static_cast<char *>(seedws);
+  float *A = reinterpret_cast<float *>(w); w += pl.a;
+  float *DX = reinterpret_cast<float *>(w); w += pl.dx;
+  float *S = reinterpret_cast<float *>(w);
+  const int H = (rbf && increments) ? 2 : 1;
+  const long long rows = (long long)t * lt * H;
+  if (rows > 0x7fffffffLL) return GPSIG_EUNSUPPORTED;
+  hipLaunchKernelGGL(tvs_wide_prep_kernel, dim3((unsigned)(((long long)lt * t + 255) / 256)), dim3(256), 0, s, Z, lt, t,
+                     d, increments, Zw);
+  hipLaunchKernelGGL(tvs_seed_a_kernel, dim3((unsigned)((rows * d + 255) / 256)), dim3(256), 0, s, Z, lt, t, d,
+                     increments, H, rbf ? 0 : 1, A);
+  for (int n0 = 0; n0 < n; n0 += pl.nc) {
+    const int nc = n - n0 < pl.nc ? n - n0 : pl.nc;
+    const long long cols = (long long)(l - 1) * nc;
+    if (cols > 0x7fffffffLL) return GPSIG_EUNSUPPORTED;
+    hipLaunchKernelGGL(tvs_seed_dx_kernel, dim3((unsigned)((cols * d + 255) / 256)), dim3(256), 0, s, X, l, d, n0, nc, DX);
+    int rc = gemm_f32(s, false, true, (int)rows, (int)cols, d, 1.0f, A, d, 0, DX, d, 0, 0.0f, S, cols, 0, 1, 0, 0,
+                      nullptr, 0);
+    if (rc) return rc;
+    TvsWideArgs a{Zw, Ft, t, n, l, d, out, state, S, cols, n0, nc};
+    switch (M) {
+      case 1: rc = launch_tvs_wide<1>(a, increments, rbf, s); break;
+      case 2: rc = launch_tvs_wide<2>(a, increments, rbf, s); break;
+      case 3: rc = launch_tvs_wide<3>(a, increments, rbf, s); break;
+      case 4: rc = launch_tvs_wide<4>(a, increments, rbf, s); break;
+      case 5: rc = launch_tvs_wide<5>(a, increments, rbf, s); break;
+      case 6: rc = launch_tvs_wide<6>(a, increments, rbf, s); break;
+      case 7: rc = launch_tvs_wide<7>(a, increments, rbf, s); break;
+      default: rc = launch_tvs_wide<8>(a, increments, rbf, s); break;
+    }
+    if (rc) return rc;
   }
+  return GPSIG_OK;
 }
 
 template <int DP, int M, bool INCR>

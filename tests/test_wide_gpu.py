@@ -182,7 +182,7 @@ def test_wide_vjp_other_seeds(base, difference):
 
 
 # ----------------------------------------------------------------------------- inducing tensors
-@pytest.mark.parametrize("D,L", [(46, 136), (126, 136), (46, 500)])
+@pytest.mark.parametrize("D,L", [(46, 136), (126, 136), (46, 500), (9, 33), (12, 40)])
 @pytest.mark.parametrize("increments", [False, True])
 def test_wide_tens_vs_seq(D, L, increments):
     """K_tens_vs_seq raw levels (the wide port of the packed recursion) vs the oracle at the runners'
