@@ -27,6 +27,11 @@ struct TvsBwdWideArgs {
   const float *state;  // optional (T, n, LT)
   int n0, nc;          // this launch's sequences [n0, n0 + nc)
   float *W0, *W1;      // point weights [(k T + t)][(s nc + n - n0)]
+  // seed tiles of the chunk (matrix-core GEMMs): rows ((k T + t) H + h), w_{k,t,0} = z0 (RBF) or the linear
+  // seed's w, w_{k,t,1} = dz (RBF increments, H = 2);  SD[row][s nc + j] = <w, dx_{n0+j,s}>,
+  // SX[row][s nc + j] = <w, x_{n0+j,s}>
+  const float *SD, *SX;
+  long long sdl, sxl;
 };
 
 __host__ __device__ inline long long tvsw_zs(int d, int lt, bool incr) { return (long long)(incr ? 2 * d + 1 : d) * lt; }
@@ -58,21 +63,37 @@ template <int I, int MMAX, bool INCR, bool RBF, bool DIFF>
 __device__ __forceinline__ void tvsw_level(const TvsBwdWideArgs &a) {
   constexpr int KB = I * (I - 1) / 2;
   constexpr int LTM = MMAX * (MMAX + 1) / 2;
+  constexpr int H = (RBF && INCR) ? 2 : 1;
+  constexpr int ANCHOR = 32;
   constexpr float NHL2E = -0.72134752044448170f, L2E = 1.4426950408889634f;
   const int lane = threadIdx.x;
   const int tt = blockIdx.y;
   const int n = a.n, d = a.d, FC = 2 * d + 3, T = a.t, L = a.l, LT = a.lt;
   const int sl = blockIdx.x * 64 + lane;  // sequence within the launch's chunk
   const bool valid = sl < a.nc;
-  const int sq = a.n0 + (valid ? sl : a.nc - 1);
+  const int slc = valid ? sl : a.nc - 1;
+  const int sq = a.n0 + slc;
   cfloat *z0 = as_const(a.Zw) + (long long)tt * tvsw_zs(d, LT, INCR) + KB;  // channel q, component c: z0[q LT + c]
   cfloat *dz = z0 + (long long)d * LT;
   cfloat *hdz = z0 + (long long)2 * d * LT;
   auto ft = [&](int s, int c) { return a.Ft[((long long)s * FC + c) * n + sq]; };
   auto em1 = [](float v) { return __builtin_fabsf(v) < EM1_TAU ? em1_small(v) : __builtin_amdgcn_exp2f(v * L2E) - 1.0f; };
+  // the step dots from the seed tiles: <w_{c,h}, dx_s> (SD) and <w_{c,h}, x_s> (SX)
+  const float *sd = a.SD + ((long long)KB * T + tt) * H * a.sdl + slc;
+  const float *sx = a.SX + ((long long)KB * T + tt) * H * a.sxl + slc;
+  auto dxdot = [&](int c, int h, int s) { return sd[((long long)c * T * H + h) * a.sdl + (long long)s * a.nc]; };
+  auto xdot = [&](int c, int h, int s) { return sx[((long long)c * T * H + h) * a.sxl + (long long)s * a.nc]; };
+  float zdz[I];  // <z0, dz> of each component (RBF increments)
+#pragma unroll
+  for (int c = 0; c < I; ++c) zdz[c] = 0.f;
+  if constexpr (RBF && INCR) {
+    for (int q = 0; q < d; ++q)
+#pragma unroll
+      for (int c = 0; c < I; ++c) zdz[c] = __builtin_fmaf(z0[(long long)q * LT + c], dz[(long long)q * LT + c], zdz[c]);
+  }
 
-  // point values of the level's components at x_s: RBF k(z0, x_s) [and k(z1, x_s)]; linear <w, x_s>
-  auto pvals = [&](int s, float (&v0)[I], float (&v1)[I]) {
+  // exact point values of the level's components at x_s: RBF k(z0, x_s) [and k(z1, x_s)] (the anchors)
+  auto pexact = [&](int s, float (&v0)[I], float (&v1)[I]) {
     float e0[I], e1[I];
 #pragma unroll
     for (int c = 0; c < I; ++c) e0[c] = e1[c] = 0.f;
@@ -80,117 +101,135 @@ __device__ __forceinline__ void tvsw_level(const TvsBwdWideArgs &a) {
       const float xv = ft(s, q);
 #pragma unroll
       for (int c = 0; c < I; ++c) {
-        if constexpr (RBF) {
-          const float d0 = z0[(long long)q * LT + c] - xv;
-          e0[c] = __builtin_fmaf(d0, d0, e0[c]);
-          if constexpr (INCR) {
-            const float d1 = d0 + dz[(long long)q * LT + c];
-            e1[c] = __builtin_fmaf(d1, d1, e1[c]);
-          }
-        } else {
-          e0[c] = __builtin_fmaf(INCR ? dz[(long long)q * LT + c] : z0[(long long)q * LT + c], xv, e0[c]);
+        const float d0 = z0[(long long)q * LT + c] - xv;
+        e0[c] = __builtin_fmaf(d0, d0, e0[c]);
+        if constexpr (INCR) {
+          const float d1 = d0 + dz[(long long)q * LT + c];
+          e1[c] = __builtin_fmaf(d1, d1, e1[c]);
         }
       }
     }
 #pragma unroll
     for (int c = 0; c < I; ++c) {
+      v0[c] = __builtin_amdgcn_exp2f(e0[c] * NHL2E);
+      v1[c] = INCR ? __builtin_amdgcn_exp2f(e1[c] * NHL2E) : 0.f;
+    }
+  };
+  // p_s = <x_s - z0, dz> - |dz|^2 / 2 of each component (RBF increments): k(z1, x_s) = k(z0, x_s) e^p
+  auto pstep = [&](int s, float (&p)[I]) {
+#pragma unroll
+    for (int c = 0; c < I; ++c) p[c] = (RBF && INCR) ? xdot(c, 1, s) - zdz[c] - hdz[c] : 0.f;
+  };
+  // q_s = <z0, dx_s> - g_s (RBF: k(z0, x_{s+1}) = k(z0, x_s) e^q), c_s = <dz, dx_s>; linear: the cell itself
+  auto qstep = [&](int s, float (&qv)[I], float (&cv)[I]) {
+    const float gs = RBF ? ft(s, 2 * d + 1) : 0.f;
+#pragma unroll
+    for (int c = 0; c < I; ++c) {
+      qv[c] = dxdot(c, 0, s) - gs;
+      cv[c] = (RBF && INCR) ? dxdot(c, 1, s) : 0.f;
+    }
+  };
+  // point values from k(z0, x_s) (RBF; k(z1, x_s) = k(z0, x_s) e^p, evaluated exactly -- k(z0, x_s) refreshed
+  // too -- where some |p| > 20) or the linear point value <w, x_s>
+  auto points = [&](int s, float (&k0)[I], const float (&p)[I], float (&v0)[I], float (&v1)[I]) {
+    if constexpr (RBF && INCR) {
+      float mx = 0.f;
+#pragma unroll
+      for (int c = 0; c < I; ++c) mx = __builtin_fmaxf(mx, __builtin_fabsf(p[c]));
+      if (__builtin_amdgcn_ballot_w64(mx > 20.0f) != 0) {
+        pexact(s, k0, v1);
+#pragma unroll
+        for (int c = 0; c < I; ++c) v0[c] = k0[c];
+        return;
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < I; ++c) {
       if constexpr (RBF) {
-        v0[c] = __builtin_amdgcn_exp2f(e0[c] * NHL2E);
-        v1[c] = INCR ? __builtin_amdgcn_exp2f(e1[c] * NHL2E) : 0.f;
+        v0[c] = k0[c];
+        v1[c] = INCR ? k0[c] * __builtin_amdgcn_exp2f(p[c] * L2E) : 0.f;
       } else {
-        v0[c] = e0[c];  // the linear point value itself
+        v0[c] = xdot(c, 0, s);
         v1[c] = 0.f;
       }
     }
   };
-  // cells M_c(s) of the level (difference): from x_s, dx_s, g_s and the point values at s (c0, c1) and
-  // s + 1 (n0, n1), as sig_tvs_bwd.h cell()
-  auto cells = [&](int s, const float (&c0)[I], const float (&c1)[I], const float (&n0)[I], const float (&n1)[I],
-                   float (&m)[I]) {
-    if constexpr (!RBF) {
-      float v[I];
+  // cells M_c(s) (difference) from the step's q, c, p and the point values at s (c0, c1) and s + 1 (n0, n1)
+  auto cells = [&](const float (&qv)[I], const float (&cv)[I], const float (&p)[I], const float (&c0)[I],
+                   const float (&c1)[I], const float (&n0)[I], const float (&n1)[I], float (&m)[I]) {
 #pragma unroll
-      for (int c = 0; c < I; ++c) v[c] = 0.f;
-      for (int q = 0; q < d; ++q) {
-        const float dxv = ft(s, d + q);
-#pragma unroll
-        for (int c = 0; c < I; ++c)
-          v[c] = __builtin_fmaf(INCR ? dz[(long long)q * LT + c] : z0[(long long)q * LT + c], dxv, v[c]);
-      }
-#pragma unroll
-      for (int c = 0; c < I; ++c) m[c] = v[c];
-    } else {
-      const float gs = ft(s, 2 * d + 1);
-      float qv[I], pv[I], cv[I];
-#pragma unroll
-      for (int c = 0; c < I; ++c) {
-        qv[c] = -gs;
-        pv[c] = cv[c] = 0.f;
-      }
-      for (int q = 0; q < d; ++q) {
-        const float dxv = ft(s, d + q);
-        const float xv = INCR ? ft(s, q) : 0.f;
-#pragma unroll
-        for (int c = 0; c < I; ++c) {
-          const float zq = z0[(long long)q * LT + c];
-          qv[c] = __builtin_fmaf(zq, dxv, qv[c]);
-          if constexpr (INCR) {
-            const float dzq = dz[(long long)q * LT + c];
-            pv[c] = __builtin_fmaf(xv - zq, dzq, pv[c]);
-            cv[c] = __builtin_fmaf(dzq, dxv, cv[c]);
-          }
-        }
-      }
-#pragma unroll
-      for (int c = 0; c < I; ++c) {
-        if constexpr (!INCR) {
-          m[c] = c0[c] * em1(qv[c]);  // k(z, x_{s+1}) - k(z, x_s), any q
+    for (int c = 0; c < I; ++c) {
+      if constexpr (!RBF) {
+        m[c] = qv[c];
+      } else if constexpr (!INCR) {
+        m[c] = c0[c] * em1(qv[c]);  // k(z, x_{s+1}) - k(z, x_s), any q
+      } else {
+        const float mx = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(p[c]), __builtin_fabsf(qv[c])), __builtin_fabsf(cv[c]));
+        if (mx < EM1_TAU) {
+          const float Ep = em1_small(p[c]), Eq = em1_small(qv[c]), Ec = em1_small(cv[c]);
+          m[c] = c0[c] * __builtin_fmaf(Ep, Eq, (1.0f + Ep) * (1.0f + Eq) * Ec);
         } else {
-          const float p = pv[c] - hdz[c];
-          const float mx = __builtin_fmaxf(__builtin_fmaxf(__builtin_fabsf(p), __builtin_fabsf(qv[c])), __builtin_fabsf(cv[c]));
-          if (mx < EM1_TAU) {
-            const float Ep = em1_small(p), Eq = em1_small(qv[c]), Ec = em1_small(cv[c]);
-            m[c] = c0[c] * __builtin_fmaf(Ep, Eq, (1.0f + Ep) * (1.0f + Eq) * Ec);
-          } else {
-            m[c] = (n1[c] - n0[c]) - (c1[c] - c0[c]);
-          }
+          m[c] = (n1[c] - n0[c]) - (c1[c] - c0[c]);
         }
       }
     }
   };
-  // point values as cells (difference=False): RBF k(z0, x) [k(z1, x) - k(z0, x)], linear <w, x>
+  // point cells (difference=False): RBF k(z0, x) [k(z1, x) - k(z0, x)], linear <w, x>
   auto pcells = [&](const float (&v0)[I], const float (&v1)[I], float (&m)[I]) {
 #pragma unroll
     for (int c = 0; c < I; ++c) m[c] = RBF ? (INCR ? v1[c] - v0[c] : v0[c]) : v0[c];
+  };
+  // k(z0, x) carried along the sweep by e^{+-q}, re-evaluated exactly every ANCHOR points and wherever
+  // the step factor leaves [e^-20, e^20] (wave-uniform)
+  auto far = [](const float (&qv)[I]) {
+    float mx = 0.f;
+#pragma unroll
+    for (int c = 0; c < I; ++c) mx = __builtin_fmaxf(mx, __builtin_fabsf(qv[c]));
+    return __builtin_amdgcn_ballot_w64(mx > 20.0f) != 0;
   };
 
   const float gI = valid ? a.gout[((long long)I * T + tt) * n + sq] : 0.f;
   float A[I];
 #pragma unroll
   for (int c = 0; c < I; ++c) A[c] = 0.f;
-  float pv0[I], pv1[I];
   const int nsteps = DIFF ? L - 1 : L;
+  float k0[I], e1u[I];
   if (a.state) {
     const float *st = a.state + ((long long)tt * n + sq) * LTM + KB;
 #pragma unroll
     for (int c = 0; c + 1 < I; ++c) A[c] = st[c];
   } else {
-    if constexpr (DIFF) pvals(0, pv0, pv1);
+    // forward sweep to the end state
+    if constexpr (RBF) pexact(0, k0, e1u);
     for (int s = 0; s < nsteps; ++s) {
-      float m[I];
-      if constexpr (DIFF) {
-        float nv0[I], nv1[I];
-        pvals(s + 1, nv0, nv1);
-        cells(s, pv0, pv1, nv0, nv1, m);
+      float m[I], qv[I], cv[I], p[I], c0v[I], c1v[I];
+      const bool step = s + 1 < L;  // a cell to the next point (always for DIFF)
+      if (step) qstep(s, qv, cv);
+      pstep(s, p);
+      points(s, k0, p, c0v, c1v);
+      float k0n[I];
+      if constexpr (RBF) {
+        if (step) {
+          if ((s + 1) % ANCHOR == 0 || far(qv)) {
+            pexact(s + 1, k0n, e1u);
+          } else {
 #pragma unroll
-        for (int c = 0; c < I; ++c) {
-          pv0[c] = nv0[c];
-          pv1[c] = nv1[c];
+            for (int c = 0; c < I; ++c) k0n[c] = k0[c] * __builtin_amdgcn_exp2f(qv[c] * L2E);
+          }
         }
+      }
+      if constexpr (DIFF) {
+        float pn[I], n0v[I], n1v[I];
+        pstep(s + 1, pn);
+        points(s + 1, k0n, pn, n0v, n1v);
+        cells(qv, cv, p, c0v, c1v, n0v, n1v, m);
       } else {
-        float v0[I], v1[I];
-        pvals(s, v0, v1);
-        pcells(v0, v1, m);
+        pcells(c0v, c1v, m);
+      }
+      if constexpr (RBF) {
+        if (step)
+#pragma unroll
+          for (int c = 0; c < I; ++c) k0[c] = k0n[c];
       }
       float prev = m[0];
 #pragma unroll
@@ -221,14 +260,48 @@ __device__ __forceinline__ void tvsw_level(const TvsBwdWideArgs &a) {
     }
   };
   const int stop = nsteps - 1;
-  if constexpr (DIFF) pvals(stop + 1, pv0, pv1);  // point values at the last point
+  float pv0[I], pv1[I];  // point values at s + 1 (DIFF) / the previous point
+  int since = 0;         // points since the last exact k(z0, x)
+  {
+    const int s1 = DIFF ? stop + 1 : stop;  // the last point
+    float p[I];
+    if constexpr (RBF) pexact(s1, k0, e1u);
+    pstep(s1, p);
+    points(s1, k0, p, pv0, pv1);
+  }
   for (int s = stop; s >= 0; --s) {
-    float c0v[I], c1v[I], m[I], Ph[I], Av[I];
-    pvals(s, c0v, c1v);
-    if constexpr (DIFF)
-      cells(s, c0v, c1v, pv0, pv1, m);
-    else
+    float c0v[I], c1v[I], m[I], Ph[I], Av[I], qv[I], cv[I], p[I];
+    const bool step = DIFF || s + 1 < L;  // the cell s -> s + 1 exists
+    if (step) qstep(s, qv, cv);
+    pstep(s, p);
+    if constexpr (DIFF) {
+      // k(z0, x_s) = k(z0, x_{s+1}) e^{-q_s}
+      if constexpr (RBF) {
+        if (++since >= ANCHOR || far(qv)) {
+          pexact(s, k0, e1u);
+          since = 0;
+        } else {
+#pragma unroll
+          for (int c = 0; c < I; ++c) k0[c] *= __builtin_amdgcn_exp2f(-qv[c] * L2E);
+        }
+      }
+      points(s, k0, p, c0v, c1v);
+      cells(qv, cv, p, c0v, c1v, pv0, pv1, m);
+    } else {
+      if constexpr (RBF) {
+        if (s < stop) {  // point s from point s + 1
+          if (++since >= ANCHOR || far(qv)) {
+            pexact(s, k0, e1u);
+            since = 0;
+          } else {
+#pragma unroll
+            for (int c = 0; c < I; ++c) k0[c] *= __builtin_amdgcn_exp2f(-qv[c] * L2E);
+          }
+        }
+      }
+      points(s, k0, p, c0v, c1v);
       pcells(c0v, c1v, m);
+    }
     Av[0] = 1.0f;
 #pragma unroll
     for (int j = 1; j < I; ++j) {
@@ -278,6 +351,30 @@ __global__ __launch_bounds__(64) void tvs_bwd_wide_kernel(TvsBwdWideArgs a) {
     case 7: if constexpr (M >= 8) tvsw_level<8, M, INCR, RBF, DIFF>(a); break;
     default: break;
   }
+}
+
+// seed-GEMM operands: A[((k T + t) H + h)][q] = z0 / the linear seed's w (h = 0), dz (h = 1)
+__global__ __launch_bounds__(256) void tvsw_seed_a_kernel(const float *__restrict__ Z, int lt, int t, int d, int incr,
+                                                          int H, int lin, float *__restrict__ A) {
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long long)lt * t * H * d) return;
+  const int q = (int)(idx % d);
+  const long long r = idx / d;
+  const int h = (int)(r % H);
+  const float *z = Z + (r / H) * (incr ? 2 * d : d);
+  A[idx] = !incr ? z[q] : ((lin || h == 1) ? z[d + q] - z[q] : z[q]);
+}
+
+// DX[(s nc + j)][q] = x_{n0 + j, s + 1, q} - x_{n0 + j, s, q}
+__global__ __launch_bounds__(256) void tvsw_seed_dx_kernel(const float *__restrict__ X, int l, int d, int n0, int nc,
+                                                           float *__restrict__ DX) {
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long long)(l - 1) * nc * d) return;
+  const int q = (int)(idx % d);
+  const long long r = idx / d;
+  const int j = (int)(r % nc), s = (int)(r / nc);
+  const float *x = X + ((long long)(n0 + j) * l + s) * d + q;
+  DX[idx] = x[d] - x[0];
 }
 
 // Xc[(s nc + j)][q] = x_{n0 + j, s, q} (q < d), 1 (q = d): the chunk's points, time-major, augmented
@@ -337,11 +434,12 @@ constexpr size_t TVSW_TILE_BYTES = (size_t)1 << 30;
 
 struct TvswPlan {
   int nc;
-  size_t ft, zw, za0, za1, xc, gxc, gz, w0, w1, part;
+  size_t ft, zw, za0, za1, xc, gxc, gz, w0, w1, part, sa, sdx, sd, sx;
 };
 static TvswPlan tvsw_plan(int n, int l, int d, int lt, int t, bool incr) {
   TvswPlan p{};
-  long long nc = (long long)(TVSW_TILE_BYTES / ((size_t)lt * t * l * sizeof(float)));
+  // a chunk's tiles: the weights (W0, W1) and the seeds (SD, SX with H = 2), ~6 (lt t l) floats per sequence
+  long long nc = (long long)(TVSW_TILE_BYTES / ((size_t)lt * t * l * sizeof(float) * 6));
   nc = nc < 64 ? 64 : (nc / 64) * 64;
   if (nc > ((n + 63) / 64) * 64) nc = ((n + 63) / 64) * 64;
   p.nc = (int)nc;
@@ -358,9 +456,15 @@ static TvswPlan tvsw_plan(int n, int l, int d, int lt, int t, bool incr) {
   const size_t pb = gemm_splitk_bytes(lt * t, d + 1, (int)(l * nc));
   // gemm_f32 clamps the split of every chunk (the last, shorter one included) to this capacity
   p.part = a256(pa > pb ? pa : pb);
+  p.sa = a256((size_t)lt * t * 2 * d * sizeof(float));
+  p.sdx = a256((size_t)(l - 1) * nc * d * sizeof(float));
+  p.sd = a256((size_t)lt * t * 2 * (l - 1) * nc * sizeof(float));
+  p.sx = a256((size_t)lt * t * 2 * l * nc * sizeof(float));
   return p;
 }
-static size_t tvsw_bytes(const TvswPlan &p) { return p.ft + p.zw + p.za0 + p.za1 + p.xc + p.gxc + p.gz + p.w0 + p.w1 + p.part; }
+static size_t tvsw_bytes(const TvswPlan &p) {
+  return p.ft + p.zw + p.za0 + p.za1 + p.xc + p.gxc + p.gz + p.w0 + p.w1 + p.part + p.sa + p.sdx + p.sd + p.sx;
+}
 
 size_t tvs_bwd_wide_workspace(int n, int l, int d, int lt, int t) { return tvsw_bytes(tvsw_plan(n, l, d, lt, t, true)); }
 
@@ -394,7 +498,11 @@ int tvs_bwd_wide(const float *Z, int lt, int t, int incr, int d, const float *X,
   float *Gz = reinterpret_cast<float *>(w); w += pl.gz;
   float *W0 = reinterpret_cast<float *>(w); w += pl.w0;
   float *W1 = pl.w1 ? reinterpret_cast<float *>(w) : nullptr; w += pl.w1;
-  float *part = pl.part ? reinterpret_cast<float *>(w) : nullptr;
+  float *part = pl.part ? reinterpret_cast<float *>(w) : nullptr; w += pl.part;
+  float *SA = reinterpret_cast<float *>(w); w += pl.sa;
+  float *DXs = reinterpret_cast<float *>(w); w += pl.sdx;
+  float *SD = reinterpret_cast<float *>(w); w += pl.sd;
+  float *SX = reinterpret_cast<float *>(w);
   int rc = tvs_features_launch(X, n, l, d, Ft, s);
   if (rc) return rc;
   const long long zr = (long long)lt * t;
@@ -406,12 +514,26 @@ int tvs_bwd_wide(const float *Z, int lt, int t, int incr, int d, const float *X,
   if (rbf && incr)
     hipLaunchKernelGGL(tvsw_zaug_kernel, dim3((unsigned)((zr * (d + 1) + 255) / 256)), dim3(256), 0, s, Z, lt, t, d,
                        incr, 1, Za1);
+  const int H = (rbf && incr) ? 2 : 1;
+  hipLaunchKernelGGL(tvsw_seed_a_kernel, dim3((unsigned)((zr * H * d + 255) / 256)), dim3(256), 0, s, Z, lt, t, d, incr,
+                     H, rbf ? 0 : 1, SA);
   float *Gz0 = Gz, *Gz1 = (rbf && incr) ? Gz + zr * (d + 1) : nullptr;
   if (hipMemsetAsync(Gz, 0, (size_t)zr * (d + 1) * sizeof(float) * (Gz1 ? 2 : 1), s) != hipSuccess) return GPSIG_ELAUNCH;
   const int D1 = d + 1;
   for (int n0 = 0; n0 < n; n0 += pl.nc) {
     const int nc = n - n0 < pl.nc ? n - n0 : pl.nc;
-    TvsBwdWideArgs a{Zw, Ft, t, n, l, d, lt, gout, state, n0, nc, W0, W1 ? W1 : W0};
+    // the chunk's seeds: <w, dx_s> and <w, x_s> of every component row, one GEMM each
+    const long long cd = (long long)(l - 1) * nc, cx = (long long)l * nc;
+    hipLaunchKernelGGL(tvsw_seed_dx_kernel, dim3((unsigned)((cd * d + 255) / 256)), dim3(256), 0, s, X, l, d, n0, nc, DXs);
+    hipLaunchKernelGGL(tvsw_points_kernel, dim3((unsigned)((cx * (d + 1) + 255) / 256)), dim3(256), 0, s, X, l, d, n0,
+                       nc, Xc);
+    if ((rc = gemm_f32(s, false, true, (int)(zr * H), (int)cd, d, 1.0f, SA, d, 0, DXs, d, 0, 0.0f, SD, cd, 0, 1, 0, 0,
+                       nullptr, 0)))
+      return rc;
+    if ((rc = gemm_f32(s, false, true, (int)(zr * H), (int)cx, d, 1.0f, SA, d, 0, Xc, d + 1, 0, 0.0f, SX, cx, 0, 1, 0, 0,
+                       nullptr, 0)))
+      return rc;
+    TvsBwdWideArgs a{Zw, Ft, t, n, l, d, lt, gout, state, n0, nc, W0, W1 ? W1 : W0, SD, SX, cd, cx};
     switch (M) {
       case 1: rc = launch_tvsw<1>(a, incr, rbf, diff, s); break;
       case 2: rc = launch_tvsw<2>(a, incr, rbf, diff, s); break;
@@ -432,9 +554,7 @@ int tvs_bwd_wide(const float *Z, int lt, int t, int incr, int d, const float *X,
       return rc;
     hipLaunchKernelGGL(tvsw_gx_kernel, dim3((unsigned)(((long long)R * d + 255) / 256)), dim3(256), 0, s, Gxc, X, l, d,
                        n0, nc, rbf ? 1 : 0, gX);
-    // tensor side: [gZ | colsum] += W [X | 1] over the chunk's points
-    hipLaunchKernelGGL(tvsw_points_kernel, dim3((unsigned)(((long long)R * D1 + 255) / 256)), dim3(256), 0, s, X, l, d,
-                       n0, nc, Xc);
+    // tensor side: [gZ | colsum] += W [X | 1] over the chunk's points (Xc, built for the seeds)
     if ((rc = gemm_f32(s, false, false, (int)zr, D1, R, 1.0f, W0, R, 0, Xc, D1, 0, 1.0f, Gz0, D1, 0, 1, 0, 0, part, pl.part)))
       return rc;
     if (Gz1 && (rc = gemm_f32(s, false, false, (int)zr, D1, R, 1.0f, W1, R, 0, Xc, D1, 0, 1.0f, Gz1, D1, 0, 1, 0, 0, part, pl.part)))
