@@ -63,6 +63,11 @@ struct BwdArgs {
   float *tile;
   int tile_a0, tile_b0;
   long long tile_as, tile_ld;
+  // DIAG seed tiles of the wide VJP (sig_bwd_wide.hip wide_diag_tiles): pair a at dtile + (a - dt_a0) dt_pair,
+  // [c_ij (dt_rows x dt_ld)][<dx_i, y_j> (dt_rows x dt_ld)][per anchor row: k, expm1(q) (2 x dt_ld each)]
+  const float *dtile;
+  int dt_a0;
+  long long dt_pair, dt_rows, dt_ld;
 };
 
 // Load of a carry another lane of this wave stored earlier in the launch: served by L2 (agent scope),

@@ -75,6 +75,15 @@ __global__ __launch_bounds__(256) void sig_bwd_wide_kernel(BwdArgs p) {
   Seed seed;
   seed.init(p.wd, p.lw1, p.lw2, fx, fy, gl, l2);
   if constexpr (SEED == SEED_RBF_DIFF) seed.bound_c(nrows);
+  // DIAG: the pair's seed tiles (wide_diag_tiles) replace the channel loops of chunk() and the chunk anchors
+  bool tiled = false;
+  if constexpr (SEED == SEED_RBF_DIFF) {
+    if (diag && p.dtile) {
+      const float *base = p.dtile + (long long)(a - p.dt_a0) * p.dt_pair;
+      seed.set_tiles(base, base + p.dt_rows * p.dt_ld, base + 2 * p.dt_rows * p.dt_ld, p.dt_ld, gl);
+      tiled = true;
+    }
+  }
   bool colv[W], ptv[W];
 #pragma unroll
   for (int w = 0; w < W; ++w) {
@@ -88,10 +97,18 @@ __global__ __launch_bounds__(256) void sig_bwd_wide_kernel(BwdArgs p) {
   float(*cb)[64][2 * W] = cbuf[wave];
   auto regen = [&](int i0) {
     if constexpr (SEED == SEED_RBF_DIFF) {
-      seed.exact(fxc + i0, seed.Eq, seed.kc);
+      if (tiled)
+        seed.exact_tile(i0 / RC, seed.Eq, seed.kc);
+      else
+        seed.exact(fxc + i0, seed.Eq, seed.kc);
       seed.kcR = lane_next(seed.kc[0][0]);
+      if (tiled)
+        seed.chunk_tile(i0);
+      else
+        seed.chunk(i0);
+    } else {
+      seed.chunk(i0);
     }
-    seed.chunk(i0);
     auto one = [&](auto rr) {
       constexpr int r = decltype(rr)::value;
       if (i0 + r >= nrows) return;

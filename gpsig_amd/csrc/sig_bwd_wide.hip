@@ -35,6 +35,65 @@ __global__ __launch_bounds__(256) void emit_correct_kernel(const float *__restri
 }
 
 static size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
+
+// ---- DIAG seed tiles (RBF difference seed, order 1): per self-pair a, over the lane columns j < NC = LP W
+//   [c_ij = <dx_i, dx_j>  (RP x NC)][<dx_i, x_j>  (RP x NC)][anchor rows i = RC t: k(x_i, x_j), expm1(q_ij)]
+// with RP = the cell rows rounded up to the regeneration chunk RC, q_ij = <x_i - x_j, dx_j> - |dx_j|^2 / 2.
+// Two batched GEMMs off the wide records and one direct kernel for the anchors replace the VJP's channel
+// loops (the chunk dots and the chunk anchors) for the diagonal's N pairs.
+struct DiagTiles {
+  long long rows, ld, pair;  // RP, NC, floats per pair
+};
+static DiagTiles diag_tiles_of(int l, int W, int LP) {
+  const long long rp = (((long long)(l - 1) + GPSIG_WIDE_BWD_R - 1) / GPSIG_WIDE_BWD_R) * GPSIG_WIDE_BWD_R;
+  const long long nc = (long long)LP * W;
+  return {rp, nc, 2 * rp * nc + 2 * (rp / GPSIG_WIDE_BWD_R) * nc};
+}
+static bool diag_tiles_apply(int l, int d, int W, int LP, int seed, int order) {
+  return seed == SEED_RBF_DIFF && order == 1 && W > 0 && (long long)LP * W <= wide_lw(l) && l >= 2 && d > 0;
+}
+
+// anchor rows: thread per (pair, anchor t, column j)
+__global__ __launch_bounds__(256) void wide_diag_anchor_kernel(const float *__restrict__ R, long long sx, int d, int lw,
+                                                               int npairs, DiagTiles dt, float *__restrict__ T) {
+  const long long na = dt.rows / GPSIG_WIDE_BWD_R;
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long long)npairs * na * dt.ld) return;
+  const int j = (int)(idx % dt.ld);
+  const long long r = idx / dt.ld;
+  const int t = (int)(r % na);
+  const int a = (int)(r / na);
+  const float *rec = R + (long long)a * sx;
+  const int i = GPSIG_WIDE_BWD_R * t;
+  float s = 0.0f, qq = -rec[(long long)2 * d * lw + j];
+  for (int k = 0; k < d; ++k) {
+    const float df = rec[(long long)k * lw + i] - rec[(long long)k * lw + j];
+    s = __builtin_fmaf(df, df, s);
+    qq = __builtin_fmaf(df, rec[(long long)(d + k) * lw + j], qq);
+  }
+  constexpr float NHL2E = -0.72134752044448170f, L2E = 1.4426950408889634f;
+  float *o = T + (long long)a * dt.pair + 2 * dt.rows * dt.ld + (long long)(2 * t) * dt.ld + j;
+  o[0] = __builtin_amdgcn_exp2f(s * NHL2E);
+  o[dt.ld] = __builtin_fabsf(qq) < EM1_TAU ? em1_small(qq) : __builtin_amdgcn_exp2f(qq * L2E) - 1.0f;
+}
+
+static int wide_diag_tiles(const float *FX, long long sx, int d, int lw, int a0, int npairs, DiagTiles dt, float *T,
+                           hipStream_t s) {
+  const float *rec = FX + (long long)a0 * sx;
+  int rc;
+  // c_ij: op(A)[i][k] = dx_k[i], op(B)[k][j] = dx_k[j]
+  if ((rc = gemm_f32(s, true, false, (int)dt.rows, (int)dt.ld, d, 1.0f, rec + (long long)d * lw, lw, sx,
+                     rec + (long long)d * lw, lw, sx, 0.0f, T, dt.ld, dt.pair, npairs, 0, 0, nullptr, 0)))
+    return rc;
+  // <dx_i, x_j>
+  if ((rc = gemm_f32(s, true, false, (int)dt.rows, (int)dt.ld, d, 1.0f, rec + (long long)d * lw, lw, sx, rec, lw, sx,
+                     0.0f, T + dt.rows * dt.ld, dt.ld, dt.pair, npairs, 0, 0, nullptr, 0)))
+    return rc;
+  const long long n = (long long)npairs * (dt.rows / GPSIG_WIDE_BWD_R) * dt.ld;
+  hipLaunchKernelGGL(wide_diag_anchor_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, rec, sx, d, lw,
+                     npairs, dt, T);
+  return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
+}
 static inline long long up_prefix(long long r, long long ntb, long long k) { return r * ntb - k * r * (r - 1) / 2; }
 
 // point-weight tile budget of one chunk of x-rows
@@ -42,7 +101,7 @@ constexpr size_t WIDE_TILE_BYTES = (size_t)1 << 30;
 
 struct WidePlan {
   int rows;  // x-rows per chunk (multiple of 4)
-  size_t rec_x, rec_y, aug_x, aug_y, gx, gc, tile, part;
+  size_t rec_x, rec_y, aug_x, aug_y, gx, gc, tile, part, dtile;
 };
 
 static WidePlan wide_plan(int n1, int l1, int n2, int l2, int d, int pair_mode) {
@@ -66,11 +125,16 @@ static WidePlan wide_plan(int n1, int l1, int n2, int l2, int d, int pair_mode) 
     const size_t pr = gemm_splitk_bytes((int)(rows * l1), d + 1, (int)cols);
     const size_t pc = gemm_splitk_bytes((int)cols, d + 1, (int)(rows * l1));
     p.part = al256(pr > pc ? pr : pc);
+  } else {
+    const BwdGeo g = bwd_geometry_wide(l1);
+    if (g.W > 0) p.dtile = al256((size_t)rows * diag_tiles_of(l1, g.W, g.LP).pair * sizeof(float));
   }
   return p;
 }
 
-static size_t plan_bytes(const WidePlan &p) { return p.rec_x + p.rec_y + p.aug_x + p.aug_y + p.gx + p.gc + p.tile + p.part; }
+static size_t plan_bytes(const WidePlan &p) {
+  return p.rec_x + p.rec_y + p.aug_x + p.aug_y + p.gx + p.gc + p.tile + p.part + p.dtile;
+}
 
 // workspace of any pair mode (the query does not name one)
 size_t sig_bwd_wide_workspace(int n1, int l1, int n2, int l2, int d) {
@@ -101,7 +165,8 @@ int sig_bwd_wide(BwdArgs a, const float *X, const float *Y, int seed, void *work
   float *Gx = reinterpret_cast<float *>(w); w += pl.gx;
   float *Gc = pl.gc ? reinterpret_cast<float *>(w) : nullptr; w += pl.gc;
   float *T = reinterpret_cast<float *>(w); w += pl.tile;
-  float *part = pl.part ? reinterpret_cast<float *>(w) : nullptr;
+  float *part = pl.part ? reinterpret_cast<float *>(w) : nullptr; w += pl.part;
+  float *DT = pl.dtile ? reinterpret_cast<float *>(w) : nullptr;
   int rc = wide_records(X, n1, l1, d, FX, s);
   if (rc) return rc;
   if (pl.rec_y && (rc = wide_records(Y, n2, l2, d, FY, s))) return rc;
@@ -147,6 +212,15 @@ int sig_bwd_wide(BwdArgs a, const float *X, const float *Y, int seed, void *work
       c.tile_as = (long long)l1 * l1;
       c.tile_ld = l1;
       tcols = l1;
+      if (DT && r1 > c0 && diag_tiles_apply(l1, d, geo.W, geo.LP, seed, order)) {
+        const DiagTiles dt = diag_tiles_of(l1, geo.W, geo.LP);
+        if ((rc = wide_diag_tiles(FX, a.sx, d, a.lw1, c0, r1 - c0, dt, DT, s))) return rc;
+        c.dtile = DT;
+        c.dt_a0 = c0;
+        c.dt_pair = dt.pair;
+        c.dt_rows = dt.rows;
+        c.dt_ld = dt.ld;
+      }
     } else {
       const int ta0 = r0 / 4, ta1 = (r1 + 3) / 4;
       c.tiles_a0 = ta0;

@@ -65,6 +65,10 @@ struct RbfSeedWide {
   bool valid_last;
   bool clo = false;
   f2 cc[R][W2], pc[R];  // the chunk's c_ij and the pair-0 p_ij
+  // seed tiles of the pair (optional, DIAG VJP: wide_diag_tiles): this lane's columns of
+  // c_ij = <dx_i, dy_j> (tcc), <dx_i, y_j> (tpp), and per anchor row i = R t the exact k / expm1(q) (tke)
+  const float *tcc = nullptr, *tpp = nullptr, *tke = nullptr;
+  long long tld = 0;
 
   struct Row {
     int i;
@@ -141,6 +145,53 @@ struct RbfSeedWide {
         ko[w2][h] = __builtin_amdgcn_exp2f(e[h]);
         if (!(__builtin_fabsf(qq[w2][h]) < EM1_TAU)) Eqo[w2][h] = __builtin_amdgcn_exp2f(qq[w2][h] * L2E) - 1.0f;
       }
+    }
+  }
+
+  GPSIG_DEV void set_tiles(const float *cc, const float *pp, const float *ke, long long ld, int gl) {
+    tcc = cc + gl * W;
+    tpp = pp + gl * W;
+    tke = ke + gl * W;
+    tld = ld;
+  }
+
+  // exact k and expm1(q) of anchor row R t from the tile (as exact(fx + R t))
+  GPSIG_DEV void exact_tile(int t, f2 (&Eqo)[W2], f2 (&ko)[W2]) const {
+    const float *kr = tke + (long long)(2 * t) * tld, *er = kr + tld;
+    float kv[W], ev[W];
+#pragma unroll
+    for (int h = 0; h < W / 4; ++h) {
+      const f4u a = *reinterpret_cast<const f4u *>(kr + 4 * h), b = *reinterpret_cast<const f4u *>(er + 4 * h);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        kv[4 * h + e] = a[e];
+        ev[4 * h + e] = b[e];
+      }
+    }
+#pragma unroll
+    for (int w2 = 0; w2 < W2; ++w2) {
+      ko[w2] = (f2){kv[w2], kv[w2 + W2]};
+      Eqo[w2] = (f2){ev[w2], ev[w2 + W2]};
+    }
+  }
+
+  // chunk() from the tiles
+  GPSIG_DEV void chunk_tile(int i0) {
+    cfloat *gr = fx + (long long)(2 * d + 1) * lwx + i0;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      const float *cr = tcc + (long long)(i0 + r) * tld, *pr = tpp + (long long)(i0 + r) * tld;
+      float cv[W];
+#pragma unroll
+      for (int h = 0; h < W / 4; ++h) {
+        const f4u a = *reinterpret_cast<const f4u *>(cr + 4 * h);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) cv[4 * h + e] = a[e];
+      }
+      cv[W - 1] *= mlast;
+#pragma unroll
+      for (int w2 = 0; w2 < W2; ++w2) cc[r][w2] = (f2){cv[w2], cv[w2 + W2]};
+      pc[r] = (f2){pr[0], pr[W2]} - splat2(gr[r]);
     }
   }
 

@@ -103,7 +103,7 @@ def test_wide_seed_regimes(scale, jumps):
 
 
 # ----------------------------------------------------------------------------- gradients
-GTOL = 5e-5
+GTOL = 1e-5  # observed <= 2.2e-6 (tools/grad_err_scan.py, profiles/r4_wide_grad_err.jsonl)
 
 
 @pytest.mark.parametrize("D,L", [(46, 136), (126, 136), (46, 500), (33, 20)])

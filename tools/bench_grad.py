@@ -221,6 +221,37 @@ def bench_svgp(reps, t=500, n=50, l=500, nf=23, m=4):
                 fwd_ms=tf * 1e3, fwd_bwd_ms=tb * 1e3, grad_err=None)
 
 
+def bench_vosf_kdiag(reps, n=50, l=500, nf=23, m=5):
+    """The VOSF-truncated trainer's Kff diagonal (benchmarks/models/train_gpsig_vosf.py:102: SignatureLinear(
+    num_levels=5, order=5), minibatch 50, max_len 500, add_time: d = 24) forward and backward -- the
+    higher-order VJP's LDS-state kernel (csrc/sig_ho_bwd_lds.h) at W = 8, order 5."""
+    import gpsig_amd
+    from oracle import autodiff_ref as ar
+    d = nf + 1
+    Xnp = walks(n, l, d, 0)
+    X = torch.tensor(Xnp.reshape(n, -1), device="cuda", dtype=torch.float32)
+    G = torch.randn(n, device="cuda")
+    k = gpsig_amd.SignatureLinear(l * d, d, m, order=m, normalization=False)
+
+    def fwd():
+        with torch.no_grad():
+            k.Kdiag(X)
+
+    def fb():
+        Xg = X.detach().requires_grad_(True)
+        (k.Kdiag(Xg) * G).sum().backward()
+
+    tf, tb = timed(fwd, reps), timed(fb, reps)
+    S = 2
+    Xs = torch.tensor(Xnp[:S].reshape(S, -1), device="cuda", requires_grad=True)
+    Gs = torch.randn(S, dtype=torch.float64)
+    (k.Kdiag(Xs) * Gs.to("cuda")).sum().backward()
+    Xr = torch.tensor(Xnp[:S], requires_grad=True)
+    (ar.k_seq_diag(Xr, m, "linear", True, order=m).sum(0) * Gs).sum().backward()
+    return dict(path="vosf_kdiag", workload=f"SignatureLinear(num_levels={m}, order={m}) Kdiag N={n} L={l} D={d}",
+                fwd_ms=tf * 1e3, fwd_bwd_ms=tb * 1e3, grad_err=rel(Xs.grad.reshape(Xr.shape).cpu().numpy(), Xr.grad.numpy()))
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=5)
@@ -231,7 +262,7 @@ def main():
                 kuf_incr=lambda: bench_kuf(a.reps, increments=True), pde=lambda: bench_pde(a.reps),
                 pde_gram=lambda: bench_pde_gram(a.reps),
                 sig=lambda: bench_sig(a.reps), svgp46=lambda: bench_svgp(a.reps, nf=23),
-                svgp126=lambda: bench_svgp(a.reps, nf=63))
+                svgp126=lambda: bench_svgp(a.reps, nf=63), vosf_kdiag=lambda: bench_vosf_kdiag(a.reps))
     for name in todo:
         r = runs[name]()
         r["bwd_over_fwd"] = (r["fwd_bwd_ms"] - r["fwd_ms"]) / r["fwd_ms"]
