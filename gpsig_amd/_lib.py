@@ -75,7 +75,8 @@ SIGNATURES = {
     "gpsig_pde_vjp_fronts_ex": (_I, [_P, _I, _I, _P, _I, _I, _I, _I, _I, _I, _I, _I, _P, _P, _P, _P, _SZ, _P, _SZ,
                                      _P]),
     "gpsig_tens_vs_seq": (_I, [_P, _I, _I, _I, _I, _P, _I, _I, _I, _I, _I, _I, _P, _P, _SZ, _P]),
-    "gpsig_tens_gram": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P]),
+    "gpsig_tens_gram_workspace_bytes": (_SZ, [_I, _I, _I]),
+    "gpsig_tens_gram": (_I, [_P, _I, _I, _I, _I, _I, _I, _P, _P, _SZ, _P]),
     "gpsig_tens_vs_seq_vjp": (_I, [_P, _I, _I, _I, _I, _P, _I, _I, _I, _I, _I, _P, _P, _P, _P, _P, _SZ, _P]),
     "gpsig_tens_vs_seq_state": (_I, [_P, _I, _I, _I, _I, _P, _I, _I, _I, _I, _P, _P, _P, _SZ, _P]),
     "gpsig_tens_vjp_workspace_bytes": (_SZ, [_I, _I, _I]),

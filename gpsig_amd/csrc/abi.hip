@@ -9,6 +9,7 @@ namespace gpsig {
 int features(const float *X, int n, int l, int d, int DP, float *F, hipStream_t s);
 int sig_fo_launch(const SigArgs &a, int DP, int seed, long long nblocks, hipStream_t s);
 int fo_lanes_per_pair(int l2, int DP, int M, bool mf, int seed, bool split);
+void fo_wide_geo(int l2, int seed, int *W, int *LP);
 size_t fo_split_bytes(int l1, int l2, int DP, int M);
 int sig_ho_launch(const SigArgs &a, int DP, int seed, long long nblocks, hipStream_t s);
 bool ho_tiled(int d, int order);
@@ -96,8 +97,23 @@ static size_t mf_scratch(int l1, int l2, int d) {
   return d > fo_fixed_max() && wide_mf_enabled() ? align256(mf_gram_scratch_bytes(l1, l2, d)) : 0;
 }
 
+// the wide diagonal's seed tiles (wide.h DiagTiles, RBF difference seed): one chunk of pairs
+static bool diag_tiled(int n, int l, int d, int order) {
+  if (order != 1 || d <= fo_fixed_max() || n <= 0) return false;
+  int W, LP;
+  fo_wide_geo(l, SEED_RBF_DIFF, &W, &LP);
+  return (long long)LP * W >= l && diag_tiles_apply(l, d, W, LP, SEED_RBF_DIFF, 1);
+}
+static size_t diag_tile_bytes(int n, int l, int d, int order) {
+  if (!diag_tiled(n, l, d, order)) return 0;
+  int W, LP;
+  fo_wide_geo(l, SEED_RBF_DIFF, &W, &LP);
+  const DiagTiles dt = diag_tiles_of(l, W, LP);
+  return align256((size_t)diag_tile_pairs(dt, n) * dt.pair * sizeof(float));
+}
+
 extern "C" size_t gpsig_sig_workspace_bytes(int n1, int l1, int n2, int l2, int d) {
-  return feat_bytes(n1, l1, d) + feat_bytes(n2, l2, d) + mf_scratch(l1, l2, d);
+  return feat_bytes(n1, l1, d) + feat_bytes(n2, l2, d) + mf_scratch(l1, l2, d) + diag_tile_bytes(n1, l1, d, 1);
 }
 
 // The workspace of one gpsig_sig_gram / gpsig_sig_diag call: the feature records, or for the higher-order
@@ -171,7 +187,10 @@ static int sig_gram_impl(const float *X, int n1, int l1, const float *Y, int n2,
   const size_t dm_b = split ? gpsig_sig_split_bytes(l1, l2, d, num_levels) : 0;
   if (split && dm_b == 0) return GPSIG_EUNSUPPORTED;
   const size_t mc_b = mf ? mf_scratch(l1, l2, d) : 0;
-  if (!workspace || workspace_bytes < fx_b + fy_b + dm_b + mc_b) return GPSIG_EWORKSPACE;
+  const bool dtiles = wide && pair_mode == GPSIG_PAIRS_DIAG && seed == SEED_RBF_DIFF && !state &&
+                      diag_tiled(n1, l1, d, order);
+  const size_t dt_b = dtiles ? diag_tile_bytes(n1, l1, d, order) : 0;
+  if (!workspace || workspace_bytes < fx_b + fy_b + dm_b + mc_b + dt_b) return GPSIG_EWORKSPACE;
   float *FX = static_cast<float *>(workspace);
   float *FY = same ? FX : reinterpret_cast<float *>(static_cast<char *>(workspace) + fx_b);
   int rc = mf ? mf_records(X, n1, l1, d, FX, s) : wide ? wide_records(X, n1, l1, d, FX, s) : features(X, n1, l1, d, DP, FX, s);
@@ -209,6 +228,29 @@ static int sig_gram_impl(const float *X, int n1, int l1, const float *Y, int n2,
   if (mf)
     return sig_fo_mf(a, d, seed, mc_b ? reinterpret_cast<float *>(static_cast<char *>(workspace) + fx_b + fy_b) : nullptr, s);
 
+  if (dtiles) {
+    // the diagonal's pairs in chunks: their seed tiles (two batched GEMMs + the anchors), then the launch
+    int gW, gLP;
+    fo_wide_geo(l2, seed, &gW, &gLP);
+    const DiagTiles dt = diag_tiles_of(l1, gW, gLP);
+    const int cp = diag_tile_pairs(dt, n1);
+    float *T = reinterpret_cast<float *>(static_cast<char *>(workspace) + fx_b + fy_b + dm_b + mc_b);
+    a.out_lvl = n1;
+    a.dtile = T;
+    a.dt_pair = dt.pair;
+    a.dt_rows = dt.rows;
+    a.dt_ld = dt.ld;
+    for (int c0 = row_begin; c0 < row_end; c0 += cp) {
+      const int c1 = c0 + cp < row_end ? c0 + cp : row_end;
+      if ((rc = wide_diag_tiles(FX, a.sx, d, a.lw1, c0, c1 - c0, dt, T, s))) return rc;
+      SigArgs c = a;
+      c.row_begin = c0;
+      c.row_end = c1;
+      c.dt_a0 = c0;
+      if ((rc = sig_fo_launch(c, DP, seed, (c1 - c0 + 3) / 4, s))) return rc;
+    }
+    return GPSIG_OK;
+  }
   const int LP = (order == 1) ? fo_lanes_per_pair(l2, DP, num_levels, mfma, seed, split) : ho_lanes_per_pair(l2, order, num_levels);
   if (LP == 0) return GPSIG_EUNSUPPORTED;
   const int G = 64 / LP;

@@ -80,7 +80,9 @@ __global__ __launch_bounds__(256) void sig_bwd_wide_kernel(BwdArgs p) {
   if constexpr (SEED == SEED_RBF_DIFF) {
     if (diag && p.dtile) {
       const float *base = p.dtile + (long long)(a - p.dt_a0) * p.dt_pair;
-      seed.set_tiles(base, base + p.dt_rows * p.dt_ld, base + 2 * p.dt_rows * p.dt_ld, p.dt_ld, gl);
+      static_assert(DIAG_TILE_ANCHOR == RC, "the regeneration chunks start on the tile's anchor rows");
+      seed.set_tiles(base, base + p.dt_rows * p.dt_ld, base + 2 * p.dt_rows * p.dt_ld, p.dt_ld, gl, DIAG_TILE_ANCHOR,
+                     (int)(p.dt_rows / DIAG_TILE_ANCHOR));
       tiled = true;
     }
   }

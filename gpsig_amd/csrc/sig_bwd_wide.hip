@@ -36,27 +36,20 @@ __global__ __launch_bounds__(256) void emit_correct_kernel(const float *__restri
 
 static size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
 
-// ---- DIAG seed tiles (RBF difference seed, order 1): per self-pair a, over the lane columns j < NC = LP W
-//   [c_ij = <dx_i, dx_j>  (RP x NC)][<dx_i, x_j>  (RP x NC)][anchor rows i = RC t: k(x_i, x_j), expm1(q_ij)]
-// with RP = the cell rows rounded up to the regeneration chunk RC, q_ij = <x_i - x_j, dx_j> - |dx_j|^2 / 2.
-// Two batched GEMMs off the wide records and one direct kernel for the anchors replace the VJP's channel
-// loops (the chunk dots and the chunk anchors) for the diagonal's N pairs.
-struct DiagTiles {
-  long long rows, ld, pair;  // RP, NC, floats per pair
-};
-static DiagTiles diag_tiles_of(int l, int W, int LP) {
-  const long long rp = (((long long)(l - 1) + GPSIG_WIDE_BWD_R - 1) / GPSIG_WIDE_BWD_R) * GPSIG_WIDE_BWD_R;
+DiagTiles diag_tiles_of(int l, int W, int LP) {
+  const long long rp = (((long long)(l - 1) + 7) / 8) * 8;
   const long long nc = (long long)LP * W;
-  return {rp, nc, 2 * rp * nc + 2 * (rp / GPSIG_WIDE_BWD_R) * nc};
+  return {rp, nc, 2 * rp * nc + 2 * (rp / DIAG_TILE_ANCHOR) * nc};
 }
-static bool diag_tiles_apply(int l, int d, int W, int LP, int seed, int order) {
-  return seed == SEED_RBF_DIFF && order == 1 && W > 0 && (long long)LP * W <= wide_lw(l) && l >= 2 && d > 0;
+bool diag_tiles_apply(int l, int d, int W, int LP, int seed, int order) {
+  return seed == SEED_RBF_DIFF && order == 1 && W > 0 && (long long)LP * W <= wide_lw(l) && l >= 2 && d > 0 &&
+         (((long long)(l - 1) + 7) / 8) * 8 <= wide_lw(l);
 }
 
 // anchor rows: thread per (pair, anchor t, column j)
 __global__ __launch_bounds__(256) void wide_diag_anchor_kernel(const float *__restrict__ R, long long sx, int d, int lw,
                                                                int npairs, DiagTiles dt, float *__restrict__ T) {
-  const long long na = dt.rows / GPSIG_WIDE_BWD_R;
+  const long long na = dt.rows / DIAG_TILE_ANCHOR;
   const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
   if (idx >= (long long)npairs * na * dt.ld) return;
   const int j = (int)(idx % dt.ld);
@@ -64,7 +57,7 @@ __global__ __launch_bounds__(256) void wide_diag_anchor_kernel(const float *__re
   const int t = (int)(r % na);
   const int a = (int)(r / na);
   const float *rec = R + (long long)a * sx;
-  const int i = GPSIG_WIDE_BWD_R * t;
+  const int i = DIAG_TILE_ANCHOR * t;
   float s = 0.0f, qq = -rec[(long long)2 * d * lw + j];
   for (int k = 0; k < d; ++k) {
     const float df = rec[(long long)k * lw + i] - rec[(long long)k * lw + j];
@@ -77,7 +70,7 @@ __global__ __launch_bounds__(256) void wide_diag_anchor_kernel(const float *__re
   o[dt.ld] = __builtin_fabsf(qq) < EM1_TAU ? em1_small(qq) : __builtin_amdgcn_exp2f(qq * L2E) - 1.0f;
 }
 
-static int wide_diag_tiles(const float *FX, long long sx, int d, int lw, int a0, int npairs, DiagTiles dt, float *T,
+int wide_diag_tiles(const float *FX, long long sx, int d, int lw, int a0, int npairs, DiagTiles dt, float *T,
                            hipStream_t s) {
   const float *rec = FX + (long long)a0 * sx;
   int rc;
@@ -89,7 +82,7 @@ static int wide_diag_tiles(const float *FX, long long sx, int d, int lw, int a0,
   if ((rc = gemm_f32(s, true, false, (int)dt.rows, (int)dt.ld, d, 1.0f, rec + (long long)d * lw, lw, sx, rec, lw, sx,
                      0.0f, T + dt.rows * dt.ld, dt.ld, dt.pair, npairs, 0, 0, nullptr, 0)))
     return rc;
-  const long long n = (long long)npairs * (dt.rows / GPSIG_WIDE_BWD_R) * dt.ld;
+  const long long n = (long long)npairs * (dt.rows / DIAG_TILE_ANCHOR) * dt.ld;
   hipLaunchKernelGGL(wide_diag_anchor_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, rec, sx, d, lw,
                      npairs, dt, T);
   return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
@@ -110,6 +103,11 @@ static WidePlan wide_plan(int n1, int l1, int n2, int l2, int d, int pair_mode) 
   const long long cols = pair_mode == GPSIG_PAIRS_DIAG ? (long long)l1 : (long long)n2 * l2;
   long long rows = (long long)(WIDE_TILE_BYTES / ((size_t)l1 * cols * sizeof(float)));
   rows = rows < 4 ? 4 : (rows / 4) * 4;
+  const BwdGeo dg = bwd_geometry_wide(l1);
+  if (pair_mode == GPSIG_PAIRS_DIAG && dg.W > 0) {  // a chunk's pairs also fit the seed-tile budget
+    const long long tp = ((long long)diag_tile_pairs(diag_tiles_of(l1, dg.W, dg.LP), 1 << 30) / 4) * 4;
+    if (rows > tp) rows = tp < 4 ? 4 : tp;
+  }
   if (rows > ((n1 + 3) / 4) * 4) rows = ((n1 + 3) / 4) * 4;
   p.rows = (int)rows;
   p.rec_x = al256((size_t)n1 * wide_rec_floats(d, l1) * sizeof(float));
@@ -125,9 +123,8 @@ static WidePlan wide_plan(int n1, int l1, int n2, int l2, int d, int pair_mode) 
     const size_t pr = gemm_splitk_bytes((int)(rows * l1), d + 1, (int)cols);
     const size_t pc = gemm_splitk_bytes((int)cols, d + 1, (int)(rows * l1));
     p.part = al256(pr > pc ? pr : pc);
-  } else {
-    const BwdGeo g = bwd_geometry_wide(l1);
-    if (g.W > 0) p.dtile = al256((size_t)rows * diag_tiles_of(l1, g.W, g.LP).pair * sizeof(float));
+  } else if (dg.W > 0) {
+    p.dtile = al256((size_t)rows * diag_tiles_of(l1, dg.W, dg.LP).pair * sizeof(float));
   }
   return p;
 }

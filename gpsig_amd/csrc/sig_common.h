@@ -54,6 +54,10 @@ struct SigArgs {
   int tile_a0, tile_b0;
   const float *RX, *RY;
   int tile_rbf;  // the tile holds RBF difference-seed cells (level 1 closed form of the RBF kernel)
+  // DIAG seed tiles of the wide forward (wide.h DiagTiles): pair a at dtile + (a - dt_a0) dt_pair
+  const float *dtile;
+  int dt_a0;
+  long long dt_pair, dt_rows, dt_ld;
 };
 
 // Saved forward state of a first-order pair (gpsig_sig_gram_state): column sums of levels 1..M-1

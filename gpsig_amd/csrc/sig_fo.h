@@ -146,6 +146,16 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
 #endif
     if constexpr (PK && !MF && SPLIT != 2 && GPSIG_CLO) seed.bound_c(fx, nrows);
     if constexpr (WIDE && SEED == SEED_RBF_DIFF && GPSIG_CLO) seed.bound_c(nrows);
+    // DIAG: the pair's seed tiles (wide.h DiagTiles) replace the chunk dots' and the anchors' channel loops
+    bool tiled = false;
+    if constexpr (WIDE && SEED == SEED_RBF_DIFF && DIAGK) {
+      if (p.dtile && nblk == 1) {
+        const float *base = p.dtile + (long long)(a - p.dt_a0) * p.dt_pair;
+        seed.set_tiles(base, base + p.dt_rows * p.dt_ld, base + 2 * p.dt_rows * p.dt_ld, p.dt_ld, gl, DIAG_TILE_ANCHOR,
+                       (int)(p.dt_rows / DIAG_TILE_ANCHOR));
+        tiled = true;
+      }
+    }
 
     f2 C[M][W2];
 #pragma unroll
@@ -272,7 +282,14 @@ __global__ GPSIG_FO_BOUNDS void sig_fo_kernel(SigArgs p) {
       if constexpr (WIDE) {
         // chunks of WIDE_R rows: one channel loop for their dots, then the rows (compile-time slots)
         for (; i < nrows; i += WIDE_R) {
-          seed.chunk(i);
+          if constexpr (SEED == SEED_RBF_DIFF) {
+            if (tiled)
+              seed.chunk_tile(i);
+            else
+              seed.chunk(i);
+          } else {
+            seed.chunk(i);
+          }
           auto one = [&](auto rr) {
             constexpr int r = decltype(rr)::value;
             if (i + r < nrows) {

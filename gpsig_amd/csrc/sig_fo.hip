@@ -95,6 +95,12 @@ int sig_fo_launch(const SigArgs &a0, int DP, int seed, long long nblocks, hipStr
 int fo_lanes_per_pair(int l2, int DP, int M, bool mf, int seed, bool split) {
   return (DP == 0 ? fo_geometry_wide(l2, seed) : fo_geometry(l2, DP, M, mf, split ? -1 : seed)).LP;
 }
+// the wide forward's (columns per lane, lanes per pair)
+void fo_wide_geo(int l2, int seed, int *W, int *LP) {
+  const Geo g = fo_geometry_wide(l2, seed);
+  *W = g.W;
+  *LP = g.LP;
+}
 
 // ------------------------------------------------------------------------------------ wide records
 __global__ __launch_bounds__(256) void wide_records_kernel(const float *__restrict__ X, int n, int l, int d,

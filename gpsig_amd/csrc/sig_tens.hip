@@ -766,14 +766,29 @@ extern "C" int gpsig_tens_vs_seq_state(const float *Z, int lt, int t, int increm
   return rc == -1 ? GPSIG_EUNSUPPORTED : rc;
 }
 
+namespace gpsig {
+size_t tens_gram_mm_bytes(int lt, int t);
+int tens_gram_mm(const float *Z, int lt, int t, int incr, int d, int M, int rbf, float *out, void *workspace,
+                 size_t workspace_bytes, hipStream_t s);
+}  // namespace gpsig
+
+// Channel counts past 32 run the pair-tile kernel of the VJP (tens_vjp_mm.hip) and need a workspace.
+extern "C" size_t gpsig_tens_gram_workspace_bytes(int lt, int t, int d) {
+  if (lt <= 0 || t <= 0 || d <= 0 || dpad4(d) != 0) return 0;
+  return gpsig::tens_gram_mm_bytes(lt, t);
+}
+
 extern "C" int gpsig_tens_gram(const float *Z, int lt, int t, int increments, int d, int num_levels, int base_kind,
-                               float *out, gpsig_stream_t stream) {
+                               float *out, void *workspace, size_t workspace_bytes, gpsig_stream_t stream) {
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (!Z || !out || lt <= 0 || t <= 0 || d <= 0 || num_levels < 1) return GPSIG_EINVAL;
   if (lt != num_levels * (num_levels + 1) / 2) return GPSIG_EINVAL;
   if (num_levels > TV_MMAX) return GPSIG_EUNSUPPORTED;
   if (base_kind != GPSIG_BASE_RBF && base_kind != GPSIG_BASE_LINEAR) return GPSIG_EUNSUPPORTED;
   const int DP = dpad4(d);
+  if (DP == 0)
+    return gpsig::tens_gram_mm(Z, lt, t, increments ? 1 : 0, d, num_levels, base_kind == GPSIG_BASE_RBF ? 1 : 0, out,
+                               workspace, workspace_bytes, s);
   TgArgs a{Z, lt, t, d, num_levels, increments, base_kind == GPSIG_BASE_RBF, out};
   dim3 grid((t + 255) / 256, t);
   switch (DP) {

@@ -134,11 +134,13 @@ __global__ __launch_bounds__(256) void tgv_pair_kernel(TgvArgs a) {
         } else {
           mv = (k11 - k10) - (k01 - k00);
         }
-        float *kv = a.kv + (long long)k * 4 * T2 + o;
-        kv[0] = k11;
-        kv[T2] = k10;
-        kv[2 * T2] = k00;
-        kv[3 * T2] = k01;
+        if (a.kv) {  // the VJP's corner kernels (the forward Gram needs m only)
+          float *kv = a.kv + (long long)k * 4 * T2 + o;
+          kv[0] = k11;
+          kv[T2] = k10;
+          kv[2 * T2] = k00;
+          kv[3 * T2] = k01;
+        }
       } else if constexpr (RBF) {
         mv = fast_exp(-0.5f * s2[i][j]);
       } else {
@@ -233,6 +235,21 @@ __global__ __launch_bounds__(256) void tgv_emit_kernel(const float *__restrict__
   gZ[idx] += v;
 }
 
+// out[i][t][t'] = prod of the level's component kernels (out[0] = 1): the forward Gram from the pair tiles
+__global__ __launch_bounds__(256) void tgv_levels_kernel(const float *__restrict__ m, int T, int M,
+                                                         float *__restrict__ out) {
+  const long long T2 = (long long)T * T;
+  const long long o = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (o >= T2) return;
+  out[o] = 1.0f;
+  int k = 0;
+  for (int i = 1; i <= M; ++i) {
+    float prod = 1.0f;
+    for (int st = 0; st < i; ++st, ++k) prod = st == 0 ? m[(long long)k * T2 + o] : m[(long long)k * T2 + o] * prod;
+    out[(long long)i * T2 + o] = prod;
+  }
+}
+
 size_t al256(size_t b) { return (b + 255) & ~(size_t)255; }
 
 struct TgvPlan {
@@ -255,6 +272,30 @@ TgvPlan tgv_plan(int lt, int t, int incr, int d, int rbf) {
 size_t tens_gram_vjp_mm_bytes(int lt, int t, int incr, int d, int rbf) {
   const TgvPlan p = tgv_plan(lt, t, incr, d, rbf);
   return p.m + p.kv + p.P + p.G;
+}
+
+size_t tens_gram_mm_bytes(int lt, int t) { return al256((size_t)lt * t * t * sizeof(float)); }
+
+// The forward tensor Gram past 32 channels: the VJP's pair-tile kernel (component kernels over all channels
+// staged through LDS) and the level products
+int tens_gram_mm(const float *Z, int lt, int t, int incr, int d, int M, int rbf, float *out, void *workspace,
+                 size_t workspace_bytes, hipStream_t s) {
+  if (M > TG_MMAX) return GPSIG_EUNSUPPORTED;
+  if (!workspace || workspace_bytes < tens_gram_mm_bytes(lt, t)) return GPSIG_EWORKSPACE;
+  if ((t + TG_TS - 1) / TG_TS > 65535 || lt > 65535) return GPSIG_EUNSUPPORTED;
+  float *m = static_cast<float *>(workspace);
+  const int mode = (incr ? 1 : 0) | (rbf ? 2 : 0);
+  TgvArgs pa{Z, t, d, incr ? 2 * d : d, lt, m, nullptr};
+  const dim3 tg((t + TG_TS - 1) / TG_TS, (t + TG_TS - 1) / TG_TS, lt);
+  switch (mode) {
+    case 0: hipLaunchKernelGGL(tgv_pair_kernel<0>, tg, dim3(256), 0, s, pa); break;
+    case 1: hipLaunchKernelGGL(tgv_pair_kernel<1>, tg, dim3(256), 0, s, pa); break;
+    case 2: hipLaunchKernelGGL(tgv_pair_kernel<2>, tg, dim3(256), 0, s, pa); break;
+    default: hipLaunchKernelGGL(tgv_pair_kernel<3>, tg, dim3(256), 0, s, pa); break;
+  }
+  const long long T2 = (long long)t * t;
+  hipLaunchKernelGGL(tgv_levels_kernel, dim3((unsigned)((T2 + 255) / 256)), dim3(256), 0, s, m, t, M, out);
+  return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
 }
 
 int tens_gram_vjp_mm(const float *Z, int lt, int t, int incr, int d, int M, int rbf, const float *gout, float *gZ,

@@ -45,6 +45,29 @@ __global__ __launch_bounds__(256) void wide_records_kernel(const float *__restri
 int wide_records(const float *X, int n, int l, int d, float *R, hipStream_t s);
 
 // ---------------------------------------------------------------------------------------------
+// Seed tiles of the diagonal's self-pairs (RBF difference seed, order 1; sig_bwd_wide.hip): per pair a,
+// over the lane columns j < NC = LP W,
+//   [c_ij = <dx_i, dx_j>  (RP x NC)][<dx_i, x_j>  (RP x NC)][anchor rows i = 4 t: k(x_i, x_j), expm1(q_ij) (2 x NC)]
+// RP = the cell rows rounded up to 8 (the forward's and the VJP's row chunks), q_ij = <x_i - x_j, dx_j> -
+// |dx_j|^2 / 2.  Two batched GEMMs off the wide records and one direct kernel for the anchors replace the
+// per-pair channel loops (the chunk dots and the anchors) of the diagonal's N pairs, which run as N waves.
+constexpr int DIAG_TILE_ANCHOR = 4;
+struct DiagTiles {
+  long long rows, ld, pair;  // RP, NC, floats per pair
+};
+DiagTiles diag_tiles_of(int l, int W, int LP);
+bool diag_tiles_apply(int l, int d, int W, int LP, int seed, int order);
+int wide_diag_tiles(const float *FX, long long sx, int d, int lw, int a0, int npairs, DiagTiles dt, float *T,
+                    hipStream_t s);
+// pairs per tile chunk (DIAG_TILE_BYTES of tiles)
+constexpr size_t DIAG_TILE_BYTES = (size_t)512 << 20;
+inline int diag_tile_pairs(const DiagTiles &dt, int n) {
+  long long p = (long long)(DIAG_TILE_BYTES / ((size_t)dt.pair * sizeof(float)));
+  if (p < 4) p = 4;
+  return (int)(p < n ? p : n);
+}
+
+// ---------------------------------------------------------------------------------------------
 // RBF difference seed on column pairs, wide channels.  Same cells and recurrences as RbfSeedPk
 // (sig_common.h); the dots of R rows come from one channel loop (chunk), the exact rows (anchor and
 // slow rows) from another.
@@ -69,6 +92,7 @@ struct RbfSeedWide {
   // c_ij = <dx_i, dy_j> (tcc), <dx_i, y_j> (tpp), and per anchor row i = R t the exact k / expm1(q) (tke)
   const float *tcc = nullptr, *tpp = nullptr, *tke = nullptr;
   long long tld = 0;
+  int tka = 1, tna = 0;  // anchor rows of the tile: i = tka t, t < tna
 
   struct Row {
     int i;
@@ -148,11 +172,13 @@ struct RbfSeedWide {
     }
   }
 
-  GPSIG_DEV void set_tiles(const float *cc, const float *pp, const float *ke, long long ld, int gl) {
+  GPSIG_DEV void set_tiles(const float *cc, const float *pp, const float *ke, long long ld, int gl, int ka, int na) {
     tcc = cc + gl * W;
     tpp = pp + gl * W;
     tke = ke + gl * W;
     tld = ld;
+    tka = ka;
+    tna = na;
   }
 
   // exact k and expm1(q) of anchor row R t from the tile (as exact(fx + R t))
@@ -235,7 +261,13 @@ struct RbfSeedWide {
     return rd;
   }
 
-  GPSIG_DEV void next_exact(const Row &rd, f2 (&Eqo)[W2], f2 (&ko)[W2]) const { exact(fx + rd.i + 1, Eqo, ko); }
+  GPSIG_DEV void next_exact(const Row &rd, f2 (&Eqo)[W2], f2 (&ko)[W2]) const {
+    const int r = rd.i + 1;
+    if (tke && r % tka == 0 && r / tka < tna)
+      exact_tile(r / tka, Eqo, ko);
+    else
+      exact(fx + r, Eqo, ko);
+  }
 
   // Cells of row rd.i into dM (RbfSeedPk::row with the chunk's dots).
   template <bool CLO = false>

@@ -610,8 +610,10 @@ def tens_gram(Z: torch.Tensor, num_levels: int, base="rbf", increments: bool = F
     Z = _f32(Z)
     lt, t, d = Z.shape[0], Z.shape[1], Z.shape[-1]
     out = torch.empty((num_levels + 1, t, t), dtype=torch.float32, device=Z.device)
+    nb = lib.gpsig_tens_gram_workspace_bytes(lt, t, d)
+    ws = workspace(Z.device, nb) if nb else None
     rc = lib.gpsig_tens_gram(Z.data_ptr(), lt, t, int(increments), d, num_levels, base_kind(base), out.data_ptr(),
-                             _stream(Z.device))
+                             _ptr(ws), ws.numel() if nb else 0, _stream(Z.device))
     L.check(rc, "gpsig_tens_gram")
     return out
 

@@ -189,8 +189,11 @@ int gpsig_tens_vs_seq(const float *Z, int lt, int t, int increments, int d, cons
                       int num_levels, int order, int base_kind, int difference, float *out, void *workspace,
                       size_t workspace_bytes, gpsig_stream_t stream);
 
+/* Tensor Gram (_K_tens, kernels.py:264-284): out (num_levels+1, T, T).  Channel counts past 32 run as pair
+ * tiles (the VJP's component-kernel tile kernel) and need the workspace the query names (0 for d <= 32). */
+size_t gpsig_tens_gram_workspace_bytes(int lt, int t, int d);
 int gpsig_tens_gram(const float *Z, int lt, int t, int increments, int d, int num_levels, int base_kind, float *out,
-                    gpsig_stream_t stream);
+                    void *workspace, size_t workspace_bytes, gpsig_stream_t stream);
 
 /* Gradient of gpsig_tens_gram (tensor_kern, signature_algs.py:76-99, over _K_tens, kernels.py:264-284):
  * gout (num_levels+1, T, T) = dLoss/d(raw per-level output); accumulates (+=) gZ (same layout as Z).
