@@ -28,8 +28,9 @@ struct TvsBwdWideArgs {
   int n0, nc;          // this launch's sequences [n0, n0 + nc)
   float *W0, *W1;      // point weights [(k T + t)][(s nc + n - n0)]
   // seed tiles of the chunk (matrix-core GEMMs): rows ((k T + t) H + h), w_{k,t,0} = z0 (RBF) or the linear
-  // seed's w, w_{k,t,1} = dz (RBF increments, H = 2);  SD[row][s nc + j] = <w, dx_{n0+j,s}>,
-  // SX[row][s nc + j] = <w, x_{n0+j,s}>
+  // seed's w, w_{k,t,1} = dz (RBF increments, H = 2);  SD[row][s nc + j] = <w, dx_{n0+j,s}>, and one row
+  // (k T + t) of SX[.][s nc + j] = <w', x_{n0+j,s}> with w' = dz (RBF increments) or w (linear; RBF without
+  // increments needs none)
   const float *SD, *SX;
   long long sdl, sxl;
 };
@@ -80,9 +81,9 @@ __device__ __forceinline__ void tvsw_level(const TvsBwdWideArgs &a) {
   auto em1 = [](float v) { return __builtin_fabsf(v) < EM1_TAU ? em1_small(v) : __builtin_amdgcn_exp2f(v * L2E) - 1.0f; };
   // the step dots from the seed tiles: <w_{c,h}, dx_s> (SD) and <w_{c,h}, x_s> (SX)
   const float *sd = a.SD + ((long long)KB * T + tt) * H * a.sdl + slc;
-  const float *sx = a.SX + ((long long)KB * T + tt) * H * a.sxl + slc;
+  const float *sx = a.SX + ((long long)KB * T + tt) * a.sxl + slc;
   auto dxdot = [&](int c, int h, int s) { return sd[((long long)c * T * H + h) * a.sdl + (long long)s * a.nc]; };
-  auto xdot = [&](int c, int h, int s) { return sx[((long long)c * T * H + h) * a.sxl + (long long)s * a.nc]; };
+  auto xdot = [&](int c, int s) { return sx[(long long)c * T * a.sxl + (long long)s * a.nc]; };
   float zdz[I];  // <z0, dz> of each component (RBF increments)
 #pragma unroll
   for (int c = 0; c < I; ++c) zdz[c] = 0.f;
@@ -118,7 +119,7 @@ __device__ __forceinline__ void tvsw_level(const TvsBwdWideArgs &a) {
   // p_s = <x_s - z0, dz> - |dz|^2 / 2 of each component (RBF increments): k(z1, x_s) = k(z0, x_s) e^p
   auto pstep = [&](int s, float (&p)[I]) {
 #pragma unroll
-    for (int c = 0; c < I; ++c) p[c] = (RBF && INCR) ? xdot(c, 1, s) - zdz[c] - hdz[c] : 0.f;
+    for (int c = 0; c < I; ++c) p[c] = (RBF && INCR) ? xdot(c, s) - zdz[c] - hdz[c] : 0.f;
   };
   // q_s = <z0, dx_s> - g_s (RBF: k(z0, x_{s+1}) = k(z0, x_s) e^q), c_s = <dz, dx_s>; linear: the cell itself
   auto qstep = [&](int s, float (&qv)[I], float (&cv)[I]) {
@@ -149,7 +150,7 @@ __device__ __forceinline__ void tvsw_level(const TvsBwdWideArgs &a) {
         v0[c] = k0[c];
         v1[c] = INCR ? k0[c] * __builtin_amdgcn_exp2f(p[c] * L2E) : 0.f;
       } else {
-        v0[c] = xdot(c, 0, s);
+        v0[c] = xdot(c, s);
         v1[c] = 0.f;
       }
     }
@@ -459,7 +460,7 @@ static TvswPlan tvsw_plan(int n, int l, int d, int lt, int t, bool incr) {
   p.sa = a256((size_t)lt * t * 2 * d * sizeof(float));
   p.sdx = a256((size_t)(l - 1) * nc * d * sizeof(float));
   p.sd = a256((size_t)lt * t * 2 * (l - 1) * nc * sizeof(float));
-  p.sx = a256((size_t)lt * t * 2 * l * nc * sizeof(float));
+  p.sx = a256((size_t)lt * t * l * nc * sizeof(float));
   return p;
 }
 static size_t tvsw_bytes(const TvswPlan &p) {
@@ -530,9 +531,13 @@ int tvs_bwd_wide(const float *Z, int lt, int t, int incr, int d, const float *X,
     if ((rc = gemm_f32(s, false, true, (int)(zr * H), (int)cd, d, 1.0f, SA, d, 0, DXs, d, 0, 0.0f, SD, cd, 0, 1, 0, 0,
                        nullptr, 0)))
       return rc;
-    if ((rc = gemm_f32(s, false, true, (int)(zr * H), (int)cx, d, 1.0f, SA, d, 0, Xc, d + 1, 0, 0.0f, SX, cx, 0, 1, 0, 0,
-                       nullptr, 0)))
-      return rc;
+    // the x-dots of the dz rows (RBF increments: every other row of SA) or of the linear seed's w
+    if ((rbf && incr) || !rbf) {
+      const float *Aw = (rbf && incr) ? SA + d : SA;
+      if ((rc = gemm_f32(s, false, true, (int)zr, (int)cx, d, 1.0f, Aw, (long long)H * d, 0, Xc, d + 1, 0, 0.0f, SX, cx,
+                         0, 1, 0, 0, nullptr, 0)))
+        return rc;
+    }
     TvsBwdWideArgs a{Zw, Ft, t, n, l, d, lt, gout, state, n0, nc, W0, W1 ? W1 : W0, SD, SX, cd, cx};
     switch (M) {
       case 1: rc = launch_tvsw<1>(a, incr, rbf, diff, s); break;
