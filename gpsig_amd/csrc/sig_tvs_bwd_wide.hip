@@ -431,7 +431,7 @@ __global__ __launch_bounds__(256) void tvsw_gz_kernel(const float *__restrict__ 
 }
 
 static size_t a256(size_t b) { return (b + 255) & ~(size_t)255; }
-constexpr size_t TVSW_TILE_BYTES = (size_t)1 << 30;
+size_t tvs_tile_budget();  // sig_tvs_pk.hip (GPSIG_TVS_TILE_BYTES)
 
 struct TvswPlan {
   int nc;
@@ -440,7 +440,7 @@ struct TvswPlan {
 static TvswPlan tvsw_plan(int n, int l, int d, int lt, int t, bool incr) {
   TvswPlan p{};
   // a chunk's tiles: the weights (W0, W1) and the seeds (SD, SX with H = 2), ~6 (lt t l) floats per sequence
-  long long nc = (long long)(TVSW_TILE_BYTES / ((size_t)lt * t * l * sizeof(float) * 6));
+  long long nc = (long long)(tvs_tile_budget() / ((size_t)lt * t * l * sizeof(float) * 6));
   nc = nc < 64 ? 64 : (nc / 64) * 64;
   if (nc > ((n + 63) / 64) * 64) nc = ((n + 63) / 64) * 64;
   p.nc = (int)nc;

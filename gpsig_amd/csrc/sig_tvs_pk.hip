@@ -13,6 +13,8 @@
 // k (and Ep) are re-evaluated exactly every ANCHOR (32) cells.  Arguments past the polynomial range take
 // expm1 = e^x - 1 (a wave-uniform branch); with increments, |q| or |c| >= 2 (far-apart corners) takes
 // the plain corner difference of directly evaluated base-kernel values.
+#include <stdlib.h>
+
 #include "gemm.h"
 #include "sig_common.h"
 
@@ -336,8 +338,13 @@ struct TvsWideArgs {
   int n0, nc;
 };
 
-// seed-tile budget of one chunk of sequences
-constexpr size_t TVS_SEED_TILE_BYTES = (size_t)1 << 30;
+// seed-tile budget of one chunk of sequences (GPSIG_TVS_TILE_BYTES overrides it: the tests force several
+// chunks; read per call, so the workspace query and the launch agree)
+size_t tvs_tile_budget() {
+  const char *e = getenv("GPSIG_TVS_TILE_BYTES");
+  const long long v = e ? atoll(e) : 0;
+  return v > 0 ? (size_t)v : (size_t)1 << 30;
+}
 
 struct TvsSeedPlan {
   int nc;
@@ -347,7 +354,7 @@ struct TvsSeedPlan {
 inline TvsSeedPlan tvs_seed_plan(int n, int l, int d, int lt, int t) {
   TvsSeedPlan p{};
   const size_t per_seq = (size_t)(l - 1) * t * lt * 2 * sizeof(float);  // H = 2: the largest tile
-  long long nc = per_seq ? (long long)(TVS_SEED_TILE_BYTES / per_seq) : n;
+  long long nc = per_seq ? (long long)(tvs_tile_budget() / per_seq) : n;
   nc = nc < 64 ? 64 : (nc / 64) * 64;
   if (nc > ((n + 63) / 64) * 64) nc = ((n + 63) / 64) * 64;
   p.nc = (int)nc;

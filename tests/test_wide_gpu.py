@@ -447,3 +447,25 @@ def test_wide_mf_column_blocks(D, L, M, base):
     sym = ops.sig_gram(t(X), None, M, base=base).cpu().numpy()
     assert (norm_rel_err(sym[1:], ref.K_seq(X)[1:], axis_levels=True) < TOL).all()
     np.testing.assert_array_equal(sym, np.swapaxes(sym, 1, 2))
+
+
+@pytest.mark.parametrize("increments", [True, False])
+def test_wide_tens_vs_seq_seed_chunks(increments, monkeypatch):
+    """Kuf forward and VJP with the seed tiles split over several chunks of sequences (GPSIG_TVS_TILE_BYTES
+    forces chunks of 64 sequences): the forward equals the one-chunk launch bit for bit, the gradients to
+    fp32 rounding (the emission GEMMs accumulate the chunks in another order)."""
+    from gpsig_amd import ops
+    M, T, N, D, L = 3, 5, 150, 40, 30
+    LT = M * (M + 1) // 2
+    rng = np.random.default_rng(77)
+    Z = t(rng.standard_normal((LT, T, 2, D) if increments else (LT, T, D)) * (2.0 / np.sqrt(D)))
+    X = t(walks(rng, N, L, D, 2.0))
+    G = torch.randn(M + 1, T, N, device=DEV)
+    out1 = ops.tens_vs_seq(Z, X, M, increments=increments)
+    gz1, gx1 = ops.tens_vs_seq_vjp(Z, X, M, G, "rbf", increments)
+    monkeypatch.setenv("GPSIG_TVS_TILE_BYTES", "65536")
+    out2 = ops.tens_vs_seq(Z, X, M, increments=increments)
+    gz2, gx2 = ops.tens_vs_seq_vjp(Z, X, M, G, "rbf", increments)
+    torch.testing.assert_close(out2, out1, rtol=0, atol=0)
+    assert norm_rel_err(gz2.cpu().numpy(), gz1.cpu().numpy()) < 1e-6
+    assert norm_rel_err(gx2.cpu().numpy(), gx1.cpu().numpy()) < 1e-6
