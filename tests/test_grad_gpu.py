@@ -265,14 +265,15 @@ def test_autograd_state_budget(monkeypatch):
 
 @pytest.mark.parametrize("base", ["rbf", "linear"])
 @pytest.mark.parametrize("increments", [False, True])
-def test_tens_vs_seq_vjp_no_difference(base, increments):
+@pytest.mark.parametrize("D", [3, 40])
+def test_tens_vs_seq_vjp_no_difference(base, increments, D):
     """difference=False inducing-tensor kernel (point values as cells): Z and X gradients of the
-    normalised K_tens_vs_seq vs fp64 autodiff."""
+    normalised K_tens_vs_seq vs fp64 autodiff (D = 40: the wide VJP on GEMM seed tiles, sig_tvs_bwd_wide.hip)."""
     import gpsig_amd
-    M, D, L, T, N = 4, 3, 17, 5, 67
+    M, L, T, N = 4, 17, 5, 67
     LT = M * (M + 1) // 2
     rng = np.random.default_rng(60)
-    Z = 0.5 * rng.standard_normal((LT, T, 2, D) if increments else (LT, T, D))
+    Z = (0.5 if D <= 8 else 2.0 / np.sqrt(D)) * rng.standard_normal((LT, T, 2, D) if increments else (LT, T, D))
     X = walks(N, L, D, 61)
     G = rng.standard_normal((T, N))
     cls = gpsig_amd.SignatureRBF if base == "rbf" else gpsig_amd.SignatureLinear
