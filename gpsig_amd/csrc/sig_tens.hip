@@ -352,6 +352,7 @@ struct TgArgs {
   float *out;  // (M+1, T, T)
 };
 
+// Channel counts up to 32 (DP = 4 .. 32); wider ones run as pair tiles (tens_vjp_mm.hip tens_gram_mm).
 template <int DP>
 __global__ __launch_bounds__(256) void tens_gram_kernel(TgArgs a) {
   const int t1 = blockIdx.y;
@@ -377,16 +378,7 @@ __global__ __launch_bounds__(256) void tens_gram_kernel(TgArgs a) {
       } else {
         // kernels.py:278  M[1,1] + M[0,0] - M[1,0] - M[0,1]
         const float *za = a.Z + (((long long)k * a.t + t1) * 2) * d, *zb = a.Z + (((long long)k * a.t + t2) * 2) * d;
-        if constexpr (DP == 0) {  // any channel count
-          if (a.rbf) {
-            v = rbf_second_diff_rt(
-                d, [&](int q) { return za[q]; }, [&](int q) { return za[d + q] - za[q]; }, [&](int q) { return zb[q]; },
-                [&](int q) { return zb[d + q] - zb[q]; });
-          } else {
-            v = 0.f;
-            for (int q = 0; q < d; ++q) v = __builtin_fmaf(za[d + q] - za[q], zb[d + q] - zb[q], v);
-          }
-        } else {
+        {
         float A0[DP], dA[DP], B0[DP], dB[DP];
 #pragma unroll
         for (int q = 0; q < DP; ++q) {
@@ -796,7 +788,7 @@ extern "C" int gpsig_tens_gram(const float *Z, int lt, int t, int increments, in
     case 8: hipLaunchKernelGGL(tens_gram_kernel<8>, grid, dim3(256), 0, s, a); break;
     case 16: hipLaunchKernelGGL(tens_gram_kernel<16>, grid, dim3(256), 0, s, a); break;
     case 32: hipLaunchKernelGGL(tens_gram_kernel<32>, grid, dim3(256), 0, s, a); break;
-    default: hipLaunchKernelGGL(tens_gram_kernel<0>, grid, dim3(256), 0, s, a); break;
+    default: return GPSIG_EUNSUPPORTED;  // past 32 channels: the pair tiles above
   }
   return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
 }
