@@ -261,3 +261,18 @@ def test_higher_order_vjp_unit_scale_long(L, base, order, M):
     (ar.k_seq(Xr, Yr, M, base, order=order) * torch.tensor(G)).sum().backward()
     assert norm_rel_err(gX.cpu().numpy(), Xr.grad.numpy()) < GTOL
     assert norm_rel_err(gY.cpu().numpy(), Yr.grad.numpy()) < GTOL
+
+
+def test_higher_order_vjp_chunked_upper_vs_rect():
+    """The LDS-state VJP over several chunks of x-rows (N = 64 sequences of 300 points: the point-weight tile
+    budget holds 44 rows per chunk): the symmetric K(X) gradient (UPPER pairs, one workgroup per pair from
+    each chunk's row window) equals the cross K(X, Y) one with Y a copy of X, dK/dX + dK/dY (RECT pairs)."""
+    from gpsig_amd import ops
+    N, L, D, M, order = 64, 300, 3, 4, 3
+    X = _walks(N, L, D, 90)
+    G = np.random.default_rng(91).standard_normal((M + 1, N, N))
+    Xt = torch.tensor(X, device=DEV, dtype=torch.float32)
+    Gt = torch.tensor(G, device=DEV, dtype=torch.float32)
+    gS, _ = ops.sig_gram_vjp(Xt, None, M, Gt, base="rbf", gout_levels=True, order=order)
+    gX, gY = ops.sig_gram_vjp(Xt, Xt.clone(), M, Gt, base="rbf", gout_levels=True, order=order)
+    assert norm_rel_err(gS.cpu().numpy(), (gX + gY).cpu().numpy()) < 1e-5
