@@ -270,22 +270,11 @@ __device__ __forceinline__ void tvsw_level(const TvsBwdWideArgs &a) {
     pstep(s1, p);
     points(s1, k0, p, pv0, pv1);
   }
-  // the step's seeds (q, c, p) of the next step down are loaded while this one is processed
-  float nq[I], ncv[I], np[I];
-  auto prefetch = [&](int s) {
-    if (DIFF || s + 1 < L) qstep(s, nq, ncv);
-    pstep(s, np);
-  };
-  prefetch(stop);
   for (int s = stop; s >= 0; --s) {
     float c0v[I], c1v[I], m[I], Ph[I], Av[I], qv[I], cv[I], p[I];
-#pragma unroll
-    for (int c = 0; c < I; ++c) {
-      qv[c] = nq[c];
-      cv[c] = ncv[c];
-      p[c] = np[c];
-    }
-    if (s > 0) prefetch(s - 1);
+    const bool step = DIFF || s + 1 < L;  // the cell s -> s + 1 exists
+    if (step) qstep(s, qv, cv);
+    pstep(s, p);
     if constexpr (DIFF) {
       // k(z0, x_s) = k(z0, x_{s+1}) e^{-q_s}
       if constexpr (RBF) {

@@ -487,22 +487,18 @@ __global__ __launch_bounds__(64) void tvs_wide_kernel(TvsWideArgs a) {
       else sc[k] = 0.f;
     }
   };
-  // two steps in flight: the seeds of steps s + 1 and s + 2 load while step s is processed
-  float sq[LT], sc[LT], aq[LT], ac[LT];
+  float sq[LT], sc[LT];
   seeds(0, sq, sc);
-  if (ncell > 1) seeds(1, aq, ac);
   for (int s = 0; s < ncell; ++s) {
     float qv[LT], cv[LT], nq[LT], ncv[LT];
-    if (s + 2 < ncell) seeds(s + 2, nq, ncv);
+    if (s + 1 < ncell) seeds(s + 1, nq, ncv);
     const float g = RBF ? ft(s, 2 * d + 1) : 0.f;
 #pragma unroll
     for (int k = 0; k < LT; ++k) {
       qv[k] = sq[k] - g;
       cv[k] = sc[k];
-      sq[k] = aq[k];
-      sc[k] = ac[k];
-      aq[k] = nq[k];
-      ac[k] = ncv[k];
+      sq[k] = nq[k];
+      sc[k] = ncv[k];
     }
     float m[LT];
     if constexpr (!RBF) {
