@@ -35,13 +35,8 @@ constexpr size_t MF_LDS_MAX = 160 * 1024;
 
 // K padding: KP = 4 KQ with KQ = 2 (mod 4), so the four K quarters of a 16x16x4 operand sit two banks
 // apart in the B image (conflict-free ds_read_b64) and every lane's A pair is 8-byte aligned.
-// GPSIG_MF_KQ=0 (A/B): the smallest even KQ instead (bank conflicts on the B-side ds_read_b64, less padding)
-int mf_kq_mode();
 __host__ __device__ inline int mf_kq(int d) {
   const int q = (d + 3) / 4;
-#if !defined(__HIP_DEVICE_COMPILE__)
-  if (mf_kq_mode() == 0) return q + (q & 1);
-#endif
   return q + ((2 - q % 4) + 4) % 4;
 }
 __host__ __device__ inline int mf_kp(int d) { return 4 * mf_kq(d); }

@@ -1,18 +1,6 @@
 // gpsig_amd -- host side of the matrix-core wide-channel Gram (sig_fo_mf.h): the GEMM operand records and the
 // pair-tile launch.
-#include <stdlib.h>
-
 #include "sig_fo_mf.h"
-
-namespace gpsig {
-int mf_kq_mode() {
-  static const int v = [] {
-    const char *e = getenv("GPSIG_MF_KQ");
-    return e ? atoi(e) : 1;
-  }();
-  return v;
-}
-}  // namespace gpsig
 
 namespace gpsig {
 
