@@ -41,28 +41,40 @@ template <bool T>
 __device__ __forceinline__ void load_tile(const float *__restrict__ X, long long ld, int R, int Kd, int r0, int k0,
                                           float (&v)[8], int t) {
   if constexpr (!T) {
-    // row-major rows r (128) x k (16): thread t -> row t & 127, k half (t >> 7) * 8
-    const int r = r0 + (t & 127), kb = k0 + (t >> 7) * 8;
-    const float *p = X + (long long)r * ld + kb;
-    const bool rok = r < R;
+    // row-major rows r (128) x k (16): thread t -> k = t & 15, rows (t >> 4) + 16 e, so a wave's load covers
+    // 4 rows x 64 contiguous bytes (a lane per row would touch 64 cache lines per instruction)
+    const int k = k0 + (t & 15), rb = r0 + (t >> 4);
+    const float *p = X + (long long)rb * ld + k;
+    const bool kok = k < Kd;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = (rok && kb + e < Kd) ? p[e] : 0.0f;
+    for (int e = 0; e < 8; ++e) v[e] = (kok && rb + 16 * e < R) ? p[(long long)16 * e * ld] : 0.0f;
   } else {
     // k-major: k (16) rows x r (128) contiguous: thread t -> k = t >> 4, r chunk (t & 15) * 8
     const int k = k0 + (t >> 4), rb = r0 + (t & 15) * 8;
     const float *p = X + (long long)k * ld + rb;
     const bool kok = k < Kd;
+    if (kok && rb + 7 < R) {
+      // two 16-byte loads (align 4: an odd ld leaves rows 4-byte aligned)
+      typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+      const f4u lo = *reinterpret_cast<const f4u *>(p), hi = *reinterpret_cast<const f4u *>(p + 4);
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = (kok && rb + e < R) ? p[e] : 0.0f;
+      for (int e = 0; e < 4; ++e) {
+        v[e] = lo[e];
+        v[4 + e] = hi[e];
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = (kok && rb + e < R) ? p[e] : 0.0f;
+    }
   }
 }
 
 template <bool T>
 __device__ __forceinline__ void store_tile(float (*S)[GBM + GPAD], const float (&v)[8], int t) {
   if constexpr (!T) {
-    const int r = t & 127, kb = (t >> 7) * 8;
+    const int k = t & 15, r = t >> 4;  // (GBM + GPAD) = 4 mod 64 banks: a wave's 16 k x 4 rows hit 64 banks
 #pragma unroll
-    for (int e = 0; e < 8; ++e) S[kb + e][r] = v[e];
+    for (int e = 0; e < 8; ++e) S[k][r + 16 * e] = v[e];
   } else {
     const int k = t >> 4, rb = (t & 15) * 8;
 #pragma unroll
@@ -123,7 +135,7 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(a[i], b[j], acc[i][j], 0, 0, 0);
+        for (int j = 0; j < 2; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(b[j], a[i], acc[i][j], 0, 0, 0);
     }
     if (more) {
       store_tile<TA>(As[buf ^ 1], va, t);
@@ -131,22 +143,39 @@ __global__ __launch_bounds__(256) void gemm_f32_kernel(GemmArgs g) {
     }
     __syncthreads();
   }
-  // C/D map of 32x32: col = lane & 31, row = (r & 3) + 8 (r >> 2) + 4 (lane >> 5)
+  // The MFMA runs with B as its first operand, so each 32 x 32 tile holds C^T: lane -> C row (lane & 31),
+  // register r -> C column 4 (lane >> 5) + 8 (r >> 2) + (r & 3).  Four consecutive registers are four
+  // consecutive columns of one row: one 16-byte store each (align 4: rows of an odd ldc are not 16-byte
+  // aligned), a quarter of the store instructions of a column-per-lane epilogue.
+  typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+  const bool plain = split || g.beta == 0.0f;
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < 2; ++i) {
+    const int row = m0 + wm + 32 * i + (lane & 31);
+    if (row >= g.M) continue;
 #pragma unroll
-    for (int j = 0; j < 2; ++j) {
-      const int col = n0 + wn + 32 * j + (lane & 31);
+    for (int j = 0; j < 2; ++j)
 #pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const int row = m0 + wm + 32 * i + (r & 3) + 8 * (r >> 2) + 4 * (lane >> 5);
-        if (row < g.M && col < g.N) {
-          float *c = C + (long long)row * ldc + col;
-          const float v = g.alpha * acc[i][j][r];
-          *c = (split || g.beta == 0.0f) ? v : __builtin_fmaf(g.beta, *c, v);
+      for (int q = 0; q < 4; ++q) {
+        const int col = n0 + wn + 32 * j + 4 * (lane >> 5) + 8 * q;
+        float *c = C + (long long)row * ldc + col;
+        f4u v;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = g.alpha * acc[i][j][4 * q + e];
+        if (col + 3 < g.N) {
+          if (!plain) {
+            const f4u o = *reinterpret_cast<const f4u *>(c);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) v[e] = __builtin_fmaf(g.beta, o[e], v[e]);
+          }
+          *reinterpret_cast<f4u *>(c) = v;
+        } else {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (col + e < g.N) c[e] = plain ? v[e] : __builtin_fmaf(g.beta, c[e], v[e]);
         }
       }
-    }
+  }
 }
 
 // C = beta C + sum of the ksplit partial products (fixed order: deterministic)
