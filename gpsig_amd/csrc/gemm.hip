@@ -41,13 +41,25 @@ template <bool T>
 __device__ __forceinline__ void load_tile(const float *__restrict__ X, long long ld, int R, int Kd, int r0, int k0,
                                           float (&v)[8], int t) {
   if constexpr (!T) {
-    // row-major rows r (128) x k (16): thread t -> k = t & 15, rows (t >> 4) + 16 e, so a wave's load covers
-    // 4 rows x 64 contiguous bytes (a lane per row would touch 64 cache lines per instruction)
-    const int k = k0 + (t & 15), rb = r0 + (t >> 4);
+    // row-major rows r (128) x k (16): thread t -> k = 4 (t & 3) .. + 3, rows (t >> 2) + 64 e, one 16-byte
+    // load per row, so a wave's load covers 16 rows x 64 contiguous bytes (a lane per row would touch 64
+    // cache lines per instruction); v[4 e + c] = (row (t >> 2) + 64 e, k + c)
+    typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));
+    const int k = k0 + 4 * (t & 3), rb = r0 + (t >> 2);
     const float *p = X + (long long)rb * ld + k;
-    const bool kok = k < Kd;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = (kok && rb + 16 * e < R) ? p[(long long)16 * e * ld] : 0.0f;
+    for (int e = 0; e < 2; ++e) {
+      const int r = rb + 64 * e;
+      const float *q = p + (long long)64 * e * ld;
+      if (r < R && k + 3 < Kd) {
+        const f4u w = *reinterpret_cast<const f4u *>(q);
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[4 * e + c] = w[c];
+      } else {
+#pragma unroll
+        for (int c = 0; c < 4; ++c) v[4 * e + c] = (r < R && k + c < Kd) ? q[c] : 0.0f;
+      }
+    }
   } else {
     // k-major: k (16) rows x r (128) contiguous: thread t -> k = t >> 4, r chunk (t & 15) * 8
     const int k = k0 + (t >> 4), rb = r0 + (t & 15) * 8;
@@ -72,9 +84,12 @@ __device__ __forceinline__ void load_tile(const float *__restrict__ X, long long
 template <bool T>
 __device__ __forceinline__ void store_tile(float (*S)[GBM + GPAD], const float (&v)[8], int t) {
   if constexpr (!T) {
-    const int k = t & 15, r = t >> 4;  // (GBM + GPAD) = 4 mod 64 banks: a wave's 16 k x 4 rows hit 64 banks
+    // (GBM + GPAD) = 4 mod 64 banks: a wave's 4 k-groups x 16 rows hit 64 distinct banks per store
+    const int k = 4 * (t & 3), r = t >> 2;
 #pragma unroll
-    for (int e = 0; e < 8; ++e) S[k][r + 16 * e] = v[e];
+    for (int e = 0; e < 2; ++e)
+#pragma unroll
+      for (int c = 0; c < 4; ++c) S[k + c][r + 64 * e] = v[4 * e + c];
   } else {
     const int k = t >> 4, rb = (t & 15) * 8;
 #pragma unroll

@@ -1,6 +1,7 @@
 #!/bin/bash
 # Round-4 A/B of the fp32 GEMM's row-major operand loads (lane per row -> 16 lanes along K per row):
-# (then the 16-byte epilogue on the transposed accumulator and 16-byte k-major loads)
+# (then the 16-byte epilogue on the transposed accumulator and 16-byte k-major loads; then 16-byte
+# row-major loads, A/B against the previous commit)
 # tools/bench_gemm.py with the previous loads (gpsig_amd/_ab/libgpsig_old.so) and the new ones, the GEMM
 # parity test, the wide / gradient suites that call the GEMM, then the SVGP step timing.
 OUT=${1:-gpurun_out/r4t}
