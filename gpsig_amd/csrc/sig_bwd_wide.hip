@@ -46,28 +46,46 @@ bool diag_tiles_apply(int l, int d, int W, int LP, int seed, int order) {
          (((long long)(l - 1) + 7) / 8) * 8 <= wide_lw(l);
 }
 
-// anchor rows: thread per (pair, anchor t, column j)
+// anchor rows: thread per (pair, group of ANCHOR_G anchor rows, column j); the pair and the group are
+// workgroup-uniform (grid y / z), so the anchor points x_i come in as scalar loads and every thread reuses its
+// column's x_j and dx_j across the group's rows
+constexpr int ANCHOR_G = 8;
 __global__ __launch_bounds__(256) void wide_diag_anchor_kernel(const float *__restrict__ R, long long sx, int d, int lw,
-                                                               int npairs, DiagTiles dt, float *__restrict__ T) {
-  const long long na = dt.rows / DIAG_TILE_ANCHOR;
-  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
-  if (idx >= (long long)npairs * na * dt.ld) return;
-  const int j = (int)(idx % dt.ld);
-  const long long r = idx / dt.ld;
-  const int t = (int)(r % na);
-  const int a = (int)(r / na);
+                                                               DiagTiles dt, float *__restrict__ T) {
+  const int na = (int)(dt.rows / DIAG_TILE_ANCHOR);
+  const int j = blockIdx.x * 256 + threadIdx.x;
+  const int t0 = blockIdx.y * ANCHOR_G, a = blockIdx.z;
+  if (j >= dt.ld) return;
   const float *rec = R + (long long)a * sx;
-  const int i = DIAG_TILE_ANCHOR * t;
-  float s = 0.0f, qq = -rec[(long long)2 * d * lw + j];
+  float s[ANCHOR_G], qq[ANCHOR_G];
+  const float q0 = -rec[(long long)2 * d * lw + j];
+#pragma unroll
+  for (int g = 0; g < ANCHOR_G; ++g) {
+    s[g] = 0.0f;
+    qq[g] = q0;
+  }
+#pragma unroll 4
   for (int k = 0; k < d; ++k) {
-    const float df = rec[(long long)k * lw + i] - rec[(long long)k * lw + j];
-    s = __builtin_fmaf(df, df, s);
-    qq = __builtin_fmaf(df, rec[(long long)(d + k) * lw + j], qq);
+    const float xj = rec[(long long)k * lw + j], dxj = rec[(long long)(d + k) * lw + j];
+    const float *xk = rec + (long long)k * lw;
+#pragma unroll
+    for (int g = 0; g < ANCHOR_G; ++g) {
+      // a group past the last anchor repeats the last one (not stored)
+      const int t = t0 + g < na ? t0 + g : na - 1;
+      const float df = xk[DIAG_TILE_ANCHOR * t] - xj;
+      s[g] = __builtin_fmaf(df, df, s[g]);
+      qq[g] = __builtin_fmaf(df, dxj, qq[g]);
+    }
   }
   constexpr float NHL2E = -0.72134752044448170f, L2E = 1.4426950408889634f;
-  float *o = T + (long long)a * dt.pair + 2 * dt.rows * dt.ld + (long long)(2 * t) * dt.ld + j;
-  o[0] = __builtin_amdgcn_exp2f(s * NHL2E);
-  o[dt.ld] = __builtin_fabsf(qq) < EM1_TAU ? em1_small(qq) : __builtin_amdgcn_exp2f(qq * L2E) - 1.0f;
+#pragma unroll
+  for (int g = 0; g < ANCHOR_G; ++g) {
+    const int t = t0 + g;
+    if (t >= na) break;
+    float *o = T + (long long)a * dt.pair + 2 * dt.rows * dt.ld + (long long)(2 * t) * dt.ld + j;
+    o[0] = __builtin_amdgcn_exp2f(s[g] * NHL2E);
+    o[dt.ld] = __builtin_fabsf(qq[g]) < EM1_TAU ? em1_small(qq[g]) : __builtin_amdgcn_exp2f(qq[g] * L2E) - 1.0f;
+  }
 }
 
 int wide_diag_tiles(const float *FX, long long sx, int d, int lw, int a0, int npairs, DiagTiles dt, float *T,
@@ -82,9 +100,11 @@ int wide_diag_tiles(const float *FX, long long sx, int d, int lw, int a0, int np
   if ((rc = gemm_f32(s, true, false, (int)dt.rows, (int)dt.ld, d, 1.0f, rec + (long long)d * lw, lw, sx, rec, lw, sx,
                      0.0f, T + dt.rows * dt.ld, dt.ld, dt.pair, npairs, 0, 0, nullptr, 0)))
     return rc;
-  const long long n = (long long)npairs * (dt.rows / DIAG_TILE_ANCHOR) * dt.ld;
-  hipLaunchKernelGGL(wide_diag_anchor_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, rec, sx, d, lw,
-                     npairs, dt, T);
+  const long long na = dt.rows / DIAG_TILE_ANCHOR;
+  if (npairs > 65535) return GPSIG_EUNSUPPORTED;
+  hipLaunchKernelGGL(wide_diag_anchor_kernel,
+                     dim3((unsigned)((dt.ld + 255) / 256), (unsigned)((na + ANCHOR_G - 1) / ANCHOR_G), (unsigned)npairs),
+                     dim3(256), 0, s, rec, sx, d, lw, dt, T);
   return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
 }
 static inline long long up_prefix(long long r, long long ntb, long long k) { return r * ntb - k * r * (r - 1) / 2; }
