@@ -445,8 +445,9 @@ __global__ __launch_bounds__(64) void tvs_wide_kernel(TvsWideArgs a) {
   cfloat *hdz = z0 + (long long)2 * d * LT;
   auto ft = [&](int s, int c) { return a.Ft[((long long)s * FC + c) * n + c0]; };
 
-  // exact k(z0_k, x_s) and (INCR) expm1(p_k), p = -<z0 - x, dz> - |dz|^2/2, for every component
-  auto exact_all = [&](int s, float (&kc)[LT], float (&Ep)[LT]) {
+  // exact k(z0_k, x_s) and (INCR) expm1(p_k), p = -<z0 - x, dz> - |dz|^2/2, for every component; e1 (INCR):
+  // |z1 - x_s|^2 = |z0 - x_s|^2 + 2 <z0 - x_s, dz> + |dz|^2
+  auto exact_all = [&](int s, float (&kc)[LT], float (&Ep)[LT], float *e1 = nullptr) {
     float s2[LT], pp[LT];
 #pragma unroll
     for (int k = 0; k < LT; ++k) s2[k] = pp[k] = 0.f;
@@ -465,6 +466,7 @@ __global__ __launch_bounds__(64) void tvs_wide_kernel(TvsWideArgs a) {
       if constexpr (INCR) {
         const float p = pp[k] - hdz[k];
         Ep[k] = __builtin_fabsf(p) < EM1_TAU ? em1_small(p) : __builtin_amdgcn_exp2f(p * L2E) - 1.0f;
+        if (e1) e1[k] = __builtin_fmaf(-2.0f, p, s2[k]);
       }
     }
   };
@@ -535,19 +537,13 @@ __global__ __launch_bounds__(64) void tvs_wide_kernel(TvsWideArgs a) {
       if (corner) {
         // increments far apart: corner differences of directly evaluated base-kernel values for the cells
         // with |q| or |c| >= TVS_CORNER (z1 = z0 + dz)
+        // e1 = |z1 - x_{s+1}|^2 from the exact pass (s2 - 2 p with p = -<z0 - x, dz> - |dz|^2/2), and
+        // e0 = |z1 - x_s|^2 = e1 + 2 <z1 - x_s, dx_s> - |dx_s|^2 = e1 + 2 (q + c) off the step's seeds
+        // (q = <z0 - x_s, dx_s> - |dx_s|^2/2, c = <dz, dx_s>): no second pass over the channels
         float kn[LT], Epn[LT], e1[LT], e0[LT];
-        exact_all(s + 1, kn, Epn);
+        exact_all(s + 1, kn, Epn, e1);
 #pragma unroll
-        for (int k = 0; k < LT; ++k) e1[k] = e0[k] = 0.f;
-        for (int q = 0; q < d; ++q) {
-          const float xs = ft(s, q), xn = ft(s + 1, q);
-#pragma unroll
-          for (int k = 0; k < LT; ++k) {
-            const float z1 = z0[(long long)q * LT + k] + dz[(long long)q * LT + k];
-            e1[k] = __builtin_fmaf(z1 - xn, z1 - xn, e1[k]);
-            e0[k] = __builtin_fmaf(z1 - xs, z1 - xs, e0[k]);
-          }
-        }
+        for (int k = 0; k < LT; ++k) e0[k] = __builtin_fmaf(2.0f, qv[k] + cv[k], e1[k]);
 #pragma unroll
         for (int k = 0; k < LT; ++k) {
           const bool ok = __builtin_fabsf(qv[k]) < TVS_CORNER && __builtin_fabsf(cv[k]) < TVS_CORNER;

@@ -199,6 +199,29 @@ def test_wide_tens_vs_seq(D, L, increments):
     assert (norm_rel_err(got[1:], exp[1:], axis_levels=True) < TOL).all()
 
 
+@pytest.mark.parametrize("D", [46, 126])
+def test_wide_tens_vs_seq_corner(D):
+    """Kuf raw levels with increments far apart: |q| or |c| >= 2 on many steps, so the forward takes the
+    corner differences of directly evaluated base-kernel values (|z1 - x|^2 from the exact pass and the
+    step's seeds) rather than the chained expm1 recurrences."""
+    from gpsig_amd import ops
+    M, T, N, L = 4, 6, 24, 60
+    LT = M * (M + 1) // 2
+    rng = np.random.default_rng(D + 7)
+    Z = rng.standard_normal((LT, T, 2, D)) * (1.0 / np.sqrt(D))
+    inc = rng.standard_normal((N, L, D)) * (1.5 / np.sqrt(D))
+    inc[:, ::7, :] *= 3.0
+    X = np.cumsum(inc, 1)
+    dx = np.diff(X, axis=1)
+    q = np.einsum("ktd,nsd->ktns", Z[:, :, 0], dx) - np.einsum("nsd,nsd->ns", X[:, :-1], dx) \
+        - 0.5 * np.einsum("nsd,nsd->ns", dx, dx)
+    assert (np.abs(q) >= 2.0).mean() > 0.1  # the corner regime is exercised
+    ref = kr.SignatureKernelRef(L * D, D, M, normalization=False)
+    exp = ref.K_tens_vs_seq_raw(Z, X, increments=True)
+    got = ops.tens_vs_seq(t(Z), t(X), M, increments=True).cpu().numpy()
+    assert (norm_rel_err(got[1:], exp[1:], axis_levels=True) < TOL).all()
+
+
 @pytest.mark.parametrize("order,difference,base", [(2, True, "rbf"), (1, False, "rbf"), (1, True, "linear"),
                                                    (3, True, "linear")])
 def test_wide_tens_vs_seq_generic(order, difference, base):
