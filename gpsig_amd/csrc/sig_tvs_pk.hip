@@ -447,7 +447,8 @@ __global__ __launch_bounds__(64) void tvs_wide_kernel(TvsWideArgs a) {
 
   // exact k(z0_k, x_s) and (INCR) expm1(p_k), p = -<z0 - x, dz> - |dz|^2/2, for every component; e1 (INCR):
   // |z1 - x_s|^2 = |z0 - x_s|^2 + 2 <z0 - x_s, dz> + |dz|^2
-  auto exact_all = [&](int s, float (&kc)[LT], float (&Ep)[LT], float *e1 = nullptr) {
+  auto exact_all = [&](int s, float (&kc)[LT], float (&Ep)[LT], float *e1 = nullptr, float *s2o = nullptr,
+                       float *ppo = nullptr) {
     float s2[LT], pp[LT];
 #pragma unroll
     for (int k = 0; k < LT; ++k) s2[k] = pp[k] = 0.f;
@@ -467,16 +468,23 @@ __global__ __launch_bounds__(64) void tvs_wide_kernel(TvsWideArgs a) {
         const float p = pp[k] - hdz[k];
         Ep[k] = __builtin_fabsf(p) < EM1_TAU ? em1_small(p) : __builtin_amdgcn_exp2f(p * L2E) - 1.0f;
         if (e1) e1[k] = __builtin_fmaf(-2.0f, p, s2[k]);
+        if (s2o) {
+          s2o[k] = s2[k];
+          ppo[k] = pp[k];
+        }
       }
     }
   };
 
   float kc[LT], Ep[LT], Ss[LT], K[M + 1];
+  // (RBF, INCR) the exponents behind kc and Ep, carried additively between exact passes: s2c = |z0 - x_s|^2
+  // (-2 q per step), ppc = -<z0 - x_s, dz> (+ c per step); the corner cells evaluate from them
+  float s2c[LT], ppc[LT];
 #pragma unroll
-  for (int k = 0; k < LT; ++k) Ss[k] = Ep[k] = kc[k] = 0.f;
+  for (int k = 0; k < LT; ++k) Ss[k] = Ep[k] = kc[k] = s2c[k] = ppc[k] = 0.f;
 #pragma unroll
   for (int i = 0; i <= M; ++i) K[i] = 0.f;
-  if constexpr (RBF) exact_all(0, kc, Ep);
+  if constexpr (RBF) exact_all(0, kc, Ep, nullptr, s2c, ppc);
 
   const int ncell = a.l - 1;
   // the step's dots from the seed tile; the next step's are in flight while this one is processed
@@ -540,8 +548,21 @@ __global__ __launch_bounds__(64) void tvs_wide_kernel(TvsWideArgs a) {
         // e1 = |z1 - x_{s+1}|^2 from the exact pass (s2 - 2 p with p = -<z0 - x, dz> - |dz|^2/2), and
         // e0 = |z1 - x_s|^2 = e1 + 2 <z1 - x_s, dx_s> - |dx_s|^2 = e1 + 2 (q + c) off the step's seeds
         // (q = <z0 - x_s, dx_s> - |dx_s|^2/2, c = <dz, dx_s>): no second pass over the channels
+        // off an anchor row the next point's exponents come from the additive carry: no channel pass
         float kn[LT], Epn[LT], e1[LT], e0[LT];
-        exact_all(s + 1, kn, Epn, e1);
+        if (anch) {
+          exact_all(s + 1, kn, Epn, e1, s2c, ppc);
+        } else {
+#pragma unroll
+          for (int k = 0; k < LT; ++k) {
+            s2c[k] = __builtin_fmaf(-2.0f, qv[k], s2c[k]);
+            ppc[k] += cv[k];
+            const float p = ppc[k] - hdz[k];
+            kn[k] = __builtin_amdgcn_exp2f(s2c[k] * NHL2E);
+            Epn[k] = __builtin_fabsf(p) < EM1_TAU ? em1_small(p) : __builtin_amdgcn_exp2f(p * L2E) - 1.0f;
+            e1[k] = __builtin_fmaf(-2.0f, p, s2c[k]);
+          }
+        }
 #pragma unroll
         for (int k = 0; k < LT; ++k) e0[k] = __builtin_fmaf(2.0f, qv[k] + cv[k], e1[k]);
 #pragma unroll
@@ -553,13 +574,15 @@ __global__ __launch_bounds__(64) void tvs_wide_kernel(TvsWideArgs a) {
           Ep[k] = Epn[k];
         }
       } else if (anch) {
-        exact_all(s + 1, kc, Ep);  // re-anchor the recurrences every ANCHOR cells
+        exact_all(s + 1, kc, Ep, nullptr, s2c, ppc);  // re-anchor the recurrences every ANCHOR cells
       } else {
 #pragma unroll
         for (int k = 0; k < LT; ++k) {
           if constexpr (INCR) {
             kc[k] = __builtin_fmaf(kc[k], Eq[k], kc[k]);
             Ep[k] = __builtin_fmaf(Ep[k], Ec[k], Ep[k] + Ec[k]);
+            s2c[k] = __builtin_fmaf(-2.0f, qv[k], s2c[k]);
+            ppc[k] += cv[k];
           } else {
             kc[k] = kc[k] + m[k];
           }
