@@ -131,12 +131,68 @@ def _ho_gram_backward(ctx, gout):
     return gXo, gYo, gso, None
 
 
+def _epilogue(Kr, sc, cfg):
+    """The normalisation epilogue of K(X) (kernels.py:431-434: jitter, division by the square roots of the
+    diagonal, sigma * variances, level sum) on raw levels, in the dtype of Kr."""
+    n = Kr.shape[1]
+    Kj = Kr + cfg["jitter"] * torch.eye(n, dtype=Kr.dtype, device=Kr.device)[None]
+    dd = torch.sqrt(torch.diagonal(Kj, dim1=1, dim2=2))
+    K = Kj / (dd[:, :, None] * dd[:, None, :]) * sc[:, None, None]
+    return K if cfg["return_levels"] else K.sum(0)
+
+
+def _ho_folded(cfg, needs_grad):
+    """Higher-order normalised K under the higher-order VJP kernel: the forward keeps the raw levels (and, for
+    K(X, X2), the raw diagonals) and the backward folds the normalisation's diagonal terms into the weights of
+    the diagonal pairs (one VJP launch, see SigGram.backward)."""
+    return needs_grad and cfg["normalization"] and cfg["order"] > 1 and cfg["num_levels"] > 1
+
+
+def _epilogue_cross(Kr, d1, d2, sc, cfg):
+    """kernels.py:457-470: K(X, X2) over the square roots of the two raw diagonals + jitter, sigma * variances."""
+    K = Kr / (torch.sqrt(d1 + cfg["jitter"])[:, :, None] * torch.sqrt(d2 + cfg["jitter"])[:, None, :])
+    K = K * sc[:, None, None]
+    return K if cfg["return_levels"] else K.sum(0)
+
+
+def _pad_last(X, length):
+    """Sequences padded to `length` points by repeating their last point: zero increments, so every signature
+    kernel value of a difference seed is unchanged."""
+    n, l, d = X.shape
+    return X if l == length else torch.cat([X, X[:, -1:].expand(n, length - l, d)], 1)
+
+
+def _unpad_grad(g, l):
+    """Gradient of the padded sequences -> of the originals (the repeats are copies of the last point)."""
+    out = g[:, :l].clone()
+    out[:, l - 1] += g[:, l:].sum(1)
+    return out
+
+
 class SigGram(torch.autograd.Function):
     """Normalised / raw signature Gram (SignatureKernel.K) with a gfx950 backward."""
 
     @staticmethod
     def forward(ctx, Xs, X2s, scale, cfg):
         M = cfg["num_levels"]
+        lengths = (Xs.shape[1],) if X2s is None else (max(Xs.shape[1], X2s.shape[1]),)
+        if _ho_folded(cfg, any(ctx.needs_input_grad[:3])) and _ho_vjp_kernel(cfg, *lengths):
+            # raw levels (and diagonals) from the kernels, the epilogue in fp64 (the backward differentiates it)
+            kw = dict(order=cfg["order"], base=cfg["base"], difference=cfg["difference"])
+            Kr = ops.sig_gram(Xs.detach(), None if X2s is None else X2s.detach(), M, **kw)
+            sc32 = scale.detach().to(torch.float32)
+            ctx.cfg = cfg
+            ctx.scale_dtype = scale.dtype
+            ctx.state = None
+            ctx.folded = True
+            if X2s is None:
+                ctx.save_for_backward(Xs, X2s, sc32, Kr, None, None)
+                return _epilogue(Kr.double(), sc32.double(), cfg).to(torch.float32)
+            d1 = ops.sig_diag(Xs.detach(), M, **kw)
+            d2 = ops.sig_diag(X2s.detach(), M, **kw)
+            ctx.save_for_backward(Xs, X2s, sc32, Kr, d1, d2)
+            return _epilogue_cross(Kr.double(), d1.double(), d2.double(), sc32.double(), cfg).to(torch.float32)
+        ctx.folded = False
         mode = L.OUT_NORM_LEVELS if cfg["return_levels"] else L.OUT_NORM_SUM
         sc32 = scale.detach().to(torch.float32)
         kw = dict(order=cfg["order"], base=cfg["base"], difference=cfg["difference"])
@@ -161,6 +217,47 @@ class SigGram(torch.autograd.Function):
     @staticmethod
     def backward(ctx, gout):
         cfg = ctx.cfg
+        if ctx.folded:
+            # dLoss/dK_m(a, b) of the epilogue in fp64, the diagonal's own term (through 1/sqrt(K_m(a, a)))
+            # included in the weight of the pair (a, a): ONE VJP launch over the upper triangle, whose two
+            # emission sides are summed in fp64 (sig_bwd_wide.hip).  Computed as separate Gram and diagonal
+            # VJPs, the two terms cancel ~270x at the VOSF trainer's shape and their fp32
+            # rounding dominated the gradient.
+            Xs, X2s, sc32, Kr, d1, d2 = ctx.saved_tensors
+            vjp = dict(base=cfg["base"], gout_levels=True, difference=cfg["difference"], order=cfg["order"])
+            M = cfg["num_levels"]
+            if X2s is None:
+                with torch.enable_grad():
+                    K64 = Kr.double().requires_grad_(True)
+                    sc = sc32.double().requires_grad_(True)
+                    gK, gsc = torch.autograd.grad(_epilogue(K64, sc, cfg), [K64, sc], gout.double())
+                gX, _ = ops.sig_gram_vjp(Xs.detach(), None, M, gK.to(torch.float32), **vjp)
+                return (gX.to(Xs.dtype) if ctx.needs_input_grad[0] else None, None,
+                        gsc.to(ctx.scale_dtype) if ctx.needs_input_grad[2] else None, None)
+            # K(X, X2): the Gram pairs and both sets of diagonal pairs in ONE upper-triangle launch over the
+            # concatenation [X; X2] (padded to a common length by repeating last points), the weights in blocks:
+            # dLoss/dK(a, b) on the X-X2 block, the diagonal terms on the diagonal, nothing else (those pairs exit
+            # at once, sig_ho_bwd_lds.h)
+            with torch.enable_grad():
+                K64, D1, D2 = (t.double().requires_grad_(True) for t in (Kr, d1, d2))
+                sc = sc32.double().requires_grad_(True)
+                gK, g1, g2, gsc = torch.autograd.grad(_epilogue_cross(K64, D1, D2, sc, cfg), [K64, D1, D2, sc],
+                                                      gout.double())
+            n1, l1 = Xs.shape[:2]
+            n2, l2 = X2s.shape[:2]
+            lm = max(l1, l2)
+            Xc = torch.cat([_pad_last(Xs.detach().to(torch.float32), lm), _pad_last(X2s.detach().to(torch.float32), lm)])
+            Gc = torch.zeros((M + 1, n1 + n2, n1 + n2), dtype=torch.float64, device=Xs.device)
+            Gc[:, :n1, n1:] = gK
+            idx1 = torch.arange(n1, device=Xs.device)
+            idx2 = torch.arange(n1, n1 + n2, device=Xs.device)
+            Gc[:, idx1, idx1] = g1
+            Gc[:, idx2, idx2] = g2
+            gXc, _ = ops.sig_gram_vjp(Xc, None, M, Gc.to(torch.float32), **vjp)
+            gX, gY = _unpad_grad(gXc[:n1], l1), _unpad_grad(gXc[n1:], l2)
+            return (gX.to(Xs.dtype) if ctx.needs_input_grad[0] else None,
+                    gY.to(X2s.dtype) if ctx.needs_input_grad[1] else None,
+                    gsc.to(ctx.scale_dtype) if ctx.needs_input_grad[2] else None, None)
         Xs, X2s, sc32, rs1, rs2 = ctx.saved_tensors
         lengths = (Xs.shape[1],) if X2s is None else (Xs.shape[1], X2s.shape[1])
         if cfg["order"] != 1 and not _ho_vjp_kernel(cfg, *lengths):

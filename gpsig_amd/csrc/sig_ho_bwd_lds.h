@@ -11,7 +11,10 @@
 //     has been used (Dh += Rh_m[x][y] P_m[x][y]), so the descending pass needs no second slab; Rh_M is the
 //     constant g_M;
 //   * the column sums CB_m (levels 1..M) follow the multipliers in the slab; their adjoints Bh_m (1..M-1)
-//     stay in registers (the kernel runs one wave per SIMD and may use the whole 512-entry register file).
+//     stay in registers (the kernel runs one wave per SIMD and may use the whole 512-entry register file),
+//     accumulated over the rows in fp64 (round 5): summed in fp32, the rounding of these running sums was
+//     the dominant error of the gradient (4e-6 unnormalised, 1.1e-5 normalised at the VOSF trainer's
+//     L = 500, against 9e-7 / 1.6e-6 in fp64).
 // This is what the VOSF-truncated trainer differentiates (benchmarks/models/train_gpsig_vosf.py:102:
 // SignatureLinear(num_levels=5, order=5), max_len 500): orders 4-5 at up to 512 points.
 #pragma once
@@ -59,6 +62,17 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void si
   }
   if (a < p.row_begin || a >= p.row_end || b >= p.n2) return;  // the whole workgroup
   const bool pair_ok = true;
+  if (p.pair_mode == GPSIG_PAIRS_UPPER && !p.rs1 && !p.gscale) {
+    // a pair without upstream gradient adds nothing (its tile rows are zeros already, sig_bwd_wide.hip): the
+    // block-structured weights of a folded cross Gram (autograd.SigGram) leave most pairs empty
+    const PairTerms<M> pt0(p, a, b, lane, true, lblk);
+    float g0[M + 1];
+    pt0.weights(g0);
+    bool any = false;
+#pragma unroll
+    for (int m = 1; m <= M; ++m) any = any || g0[m] != 0.0f;
+    if (!any) return;
+  }
   const int bl = b;
   const int l1 = p.l1, l2 = p.l2;
   const float *__restrict__ fx = p.FX + (long long)a * p.sx;
@@ -269,7 +283,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void si
   };
 
   // ---- reverse sweep
-  float Bh[Lay::nbh > 0 ? Lay::nbh : 1][W];  // dLoss/dCB_m of levels 1..M-1 (level M: the constant g_M)
+  // dLoss/dCB_m of levels 1..M-1 (level M: the constant g_M), accumulated over the rows in fp64
+  double Bh[Lay::nbh > 0 ? Lay::nbh : 1][W];
   static_for<1, M>([&](auto mt) {
     constexpr int m = decltype(mt)::value;
 #pragma unroll
@@ -354,7 +369,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void si
         for (int y = 0; y < dmv; ++y) {
           float v[W];
 #pragma unroll
-          for (int w = 0; w < W; ++w) v[w] = Bh[Lay::cbo(m) + y][w];
+          for (int w = 0; w < W; ++w) v[w] = (float)Bh[Lay::cbo(m) + y][w];
           if (x + 1 < dn) {
 #pragma unroll
             for (int w = 0; w < W; ++w) v[w] += rx1[w];
@@ -385,7 +400,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void si
         for (int y = 0; y < dmv; ++y) {
           float v[W];
 #pragma unroll
-          for (int w = 0; w < W; ++w) v[w] = Bh[Lay::cbo(m) + y][w] + rx0[w];
+          for (int w = 0; w < W; ++w) v[w] = rx0[w];
           if (y + 1 < dn) {
             float r[W];
             rh(0, y + 1, r);
@@ -393,7 +408,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void si
             for (int w = 0; w < W; ++w) v[w] = __builtin_fmaf(dM[w] * r[w], 1.0f / (float)(y + 2), v[w]);
           }
 #pragma unroll
-          for (int w = 0; w < W; ++w) Bh[Lay::cbo(m) + y][w] = v[w];
+          for (int w = 0; w < W; ++w) Bh[Lay::cbo(m) + y][w] += (double)v[w];
         }
       }
     });

@@ -180,13 +180,19 @@ __device__ __forceinline__ void tvsw_level(const TvsBwdWideArgs &a) {
 #pragma unroll
     for (int c = 0; c < I; ++c) m[c] = RBF ? (INCR ? v1[c] - v0[c] : v0[c]) : v0[c];
   };
-  // k(z0, x) carried along the sweep by e^{+-q}, re-evaluated exactly every ANCHOR points and wherever
-  // the step factor leaves [e^-20, e^20] (wave-uniform)
-  auto far = [](const float (&qv)[I]) {
+  // k(z0, x) carried along the sweep by e^{+-q} (sgn q: the exponent of this step), re-evaluated exactly every
+  // ANCHOR points, wherever the step factor leaves [e^-20, e^20], and wherever a carried value below 1e-30 is
+  // about to grow: once it has underflowed to 0 (or a denormal) the product cannot bring it back, while the
+  // exact value may have climbed to O(1) by the next anchor (wave-uniform)
+  auto far = [](const float (&qv)[I], const float (&kv)[I], float sgn) {
     float mx = 0.f;
+    bool tiny = false;
 #pragma unroll
-    for (int c = 0; c < I; ++c) mx = __builtin_fmaxf(mx, __builtin_fabsf(qv[c]));
-    return __builtin_amdgcn_ballot_w64(mx > 20.0f) != 0;
+    for (int c = 0; c < I; ++c) {
+      mx = __builtin_fmaxf(mx, __builtin_fabsf(qv[c]));
+      tiny = tiny || (kv[c] < 1e-30f && sgn * qv[c] > 0.f);
+    }
+    return __builtin_amdgcn_ballot_w64(mx > 20.0f || tiny) != 0;
   };
 
   const float gI = valid ? a.gout[((long long)I * T + tt) * n + sq] : 0.f;
@@ -211,7 +217,7 @@ __device__ __forceinline__ void tvsw_level(const TvsBwdWideArgs &a) {
       float k0n[I];
       if constexpr (RBF) {
         if (step) {
-          if ((s + 1) % ANCHOR == 0 || far(qv)) {
+          if ((s + 1) % ANCHOR == 0 || far(qv, k0, 1.0f)) {
             pexact(s + 1, k0n, e1u);
           } else {
 #pragma unroll
@@ -278,7 +284,7 @@ __device__ __forceinline__ void tvsw_level(const TvsBwdWideArgs &a) {
     if constexpr (DIFF) {
       // k(z0, x_s) = k(z0, x_{s+1}) e^{-q_s}
       if constexpr (RBF) {
-        if (++since >= ANCHOR || far(qv)) {
+        if (++since >= ANCHOR || far(qv, k0, -1.0f)) {
           pexact(s, k0, e1u);
           since = 0;
         } else {
@@ -291,7 +297,7 @@ __device__ __forceinline__ void tvsw_level(const TvsBwdWideArgs &a) {
     } else {
       if constexpr (RBF) {
         if (s < stop) {  // point s from point s + 1
-          if (++since >= ANCHOR || far(qv)) {
+          if (++since >= ANCHOR || far(qv, k0, -1.0f)) {
             pexact(s, k0, e1u);
             since = 0;
           } else {

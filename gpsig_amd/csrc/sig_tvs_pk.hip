@@ -209,6 +209,15 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(INCR ? GPSIG
           Ep[k] = Epn;
         } else if (anch) {
           exact(k, x1, kc[k], Ep[k]);  // re-anchor the recurrences every ANCHOR cells
+        } else if ((!INCR && wide && __builtin_amdgcn_ballot_w64(mx >= TVS_CORNER) != 0) ||
+                   __builtin_amdgcn_ballot_w64((kc[k][0] < 1e-30f && qv[0] > 0.f) || (kc[k][1] < 1e-30f && qv[1] > 0.f))) {
+          // exact point values instead of the carry k (1 + expm1(q)): steps with |q| >= TVS_CORNER (the
+          // rounding of q costs |q| eps of the exponent per step), and a carried k below 1e-30 about to grow
+          // (once underflowed it stays 0 while the exact value may reach O(1) before the next anchor: a path
+          // walking towards a far inducing point)
+          f2 xr[DP];
+          ldx(s + 1, xr);
+          exact(k, xr, kc[k], Ep[k]);
         } else if constexpr (INCR) {
           kc[k] = fma2(kc[k], Eq, kc[k]);
           Ep[k] = fma2(Ep[k], Ec, Ep[k] + Ec);
@@ -575,6 +584,17 @@ __global__ __launch_bounds__(64) void tvs_wide_kernel(TvsWideArgs a) {
         }
       } else if (anch) {
         exact_all(s + 1, kc, Ep, nullptr, s2c, ppc);  // re-anchor the recurrences every ANCHOR cells
+      } else if ((!INCR && wide && __builtin_amdgcn_ballot_w64(mx >= TVS_CORNER) != 0) || [&] {
+                   bool t = false;
+#pragma unroll
+                   for (int k = 0; k < LT; ++k) t = t || (kc[k] < 1e-30f && qv[k] > 0.f);
+                   return __builtin_amdgcn_ballot_w64(t) != 0;
+                 }()) {
+        // exact point values instead of the carry k (1 + expm1(q)): (a) steps with |q| >= TVS_CORNER, where
+        // the rounding of q (relative) is |q| eps in the exponent per step; (b) a carried k below 1e-30 about
+        // to grow (a path walking towards a far inducing point): once underflowed, the carry stays 0 while the
+        // exact value may reach O(1) before the next anchor
+        exact_all(s + 1, kc, Ep, nullptr, s2c, ppc);
       } else {
 #pragma unroll
         for (int k = 0; k < LT; ++k) {

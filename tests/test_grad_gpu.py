@@ -12,7 +12,7 @@ from conftest import norm_rel_err
 from oracle import autodiff_ref as ar
 
 pytestmark = pytest.mark.gpu
-GTOL = 5e-5
+GTOL = 1e-5
 DEV = "cuda"
 
 
@@ -445,3 +445,59 @@ def test_tens_vs_seq_vjp_far_inducing_point():
     (Kr * torch.tensor(G)).sum().backward()
     assert norm_rel_err(Zt.grad.cpu().numpy(), Zr.grad.numpy()) < GTOL
     assert norm_rel_err(Xt.grad.reshape(X.shape).cpu().numpy(), Xr.grad.numpy()) < GTOL
+
+
+@pytest.mark.parametrize("increments", [False, True])
+def test_wide_tens_vs_seq_vjp_path_approaching_far_point(increments):
+    """Wide channels (D = 20: the point-weight tile VJP, sig_tvs_bwd_wide.hip) with paths that start ~15
+    lengthscales from an inducing point -- k(z, x) = e^-112 underflows to 0 in fp32 -- and walk steadily
+    towards it (steps of 0.55: |q| < 20 per step, so the step-factor guard alone never fires), and paths that
+    walk away from it (the reverse sweep sees the approach).  The carried k(z, x_s) must be re-evaluated once
+    it would grow from an underflowed value, else the cells near z come out as 0."""
+    import gpsig_amd
+    M, D, L, T, N = 3, 20, 40, 3, 4
+    LT = M * (M + 1) // 2
+    rng = np.random.default_rng(80)
+    X = rng.standard_normal((N, L, D)) * 0.02
+    ramp = 15.0 - 0.55 * np.arange(L)  # channel-0 distance to z: 15 -> -6.45 (passes through z)
+    X[0, :, 0] += ramp
+    X[1, :, 0] += ramp[::-1]           # walks away (the reverse sweep approaches)
+    X[2, :, 0] += 15.0 - 0.4 * np.arange(L)
+    X[3] = np.cumsum(rng.standard_normal((L, D)) * 0.1, 0)
+    Z = rng.standard_normal((LT, T, 2, D) if increments else (LT, T, D)) * 0.1
+    Z[:, 0] *= 0.0  # the inducing points (and increments) of tensor 0 at the origin
+    G = rng.standard_normal((T, N))
+    k = gpsig_amd.SignatureRBF(L * D, D, M, normalization=False)
+    Zt = torch.tensor(Z, device=DEV, requires_grad=True)
+    Xt = torch.tensor(X.reshape(N, -1), device=DEV, requires_grad=True)
+    K = k.K_tens_vs_seq(Zt, Xt, increments=increments)
+    (K * torch.as_tensor(G, device=DEV)).sum().backward()
+    assert torch.isfinite(Zt.grad).all() and torch.isfinite(Xt.grad).all()
+    Zr, Xr = torch.tensor(Z, requires_grad=True), torch.tensor(X, requires_grad=True)
+    Kr = ar.K_tens_vs_seq(Zr, Xr, M, base="rbf", increments=increments, normalization=False)
+    assert norm_rel_err(K.detach().cpu().numpy(), Kr.detach().numpy()) < 1e-5
+    (Kr * torch.tensor(G)).sum().backward()
+    assert norm_rel_err(Zt.grad.cpu().numpy(), Zr.grad.numpy()) < GTOL
+    assert norm_rel_err(Xt.grad.reshape(X.shape).cpu().numpy(), Xr.grad.numpy()) < GTOL
+
+
+@pytest.mark.parametrize("D", [3, 20])
+def test_tens_vs_seq_forward_path_approaching_far_point(D):
+    """Forward Kuf (narrow packed kernel at D = 3, wide seed-tile kernel at D = 20) for paths that start ~15
+    lengthscales from an inducing point (k underflows to 0) and walk towards it: the carried k(z, x_s) must
+    be re-evaluated before it grows, not only at the anchors every 32 cells."""
+    import gpsig_amd
+    M, L, T, N = 3, 40, 2, 3
+    LT = M * (M + 1) // 2
+    rng = np.random.default_rng(81)
+    X = rng.standard_normal((N, L, D)) * 0.02
+    X[0, :, 0] += 15.0 - 0.55 * np.arange(L)
+    X[1, :, 0] += 15.0 - 0.3 * np.arange(L)
+    X[2] = np.cumsum(rng.standard_normal((L, D)) * 0.1, 0)
+    Z = rng.standard_normal((LT, T, D)) * 0.1
+    Z[:, 0] *= 0.0
+    k = gpsig_amd.SignatureRBF(L * D, D, M, normalization=False)
+    K = k.K_tens_vs_seq(torch.tensor(Z, device=DEV), torch.tensor(X.reshape(N, -1), device=DEV), return_levels=True)
+    Kr = ar.K_tens_vs_seq(torch.tensor(Z), torch.tensor(X), M, base="rbf", normalization=False, return_levels=True)
+    for m in range(1, M + 1):
+        assert norm_rel_err(K[m].cpu().numpy(), Kr[m].numpy()) < 1e-5, m

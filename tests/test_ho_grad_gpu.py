@@ -11,7 +11,7 @@ from conftest import golden, norm_rel_err
 from oracle import autodiff_ref as ar
 
 pytestmark = pytest.mark.gpu
-GTOL = 5e-5
+GTOL = 1e-5
 DEV = "cuda"
 
 
@@ -170,7 +170,13 @@ def test_higher_order_vjp_unsupported_raises():
 def test_higher_order_long_sequences_gradient(normalization):
     """SignatureLinear(num_levels=5, order=5) at the VOSF trainer's sequence shape (d = 24, L = 500,
     benchmarks/models/train_gpsig_vosf.py:102): K (symmetric and cross) and Kdiag gradients through the
-    LDS-state VJP kernel (W = 8 columns per lane), vs fp64 autodiff of the reference graph."""
+    LDS-state VJP kernel (W = 8 columns per lane), vs fp64 autodiff of the reference graph, plain
+    norm-relative criterion on the gradient itself.
+
+    Normalised, the Gram term and the diagonal term of the gradient cancel ~270x (the normalised kernel is
+    scale-invariant in each sequence): autograd.SigGram folds the diagonal terms into the weights of the
+    diagonal pairs of ONE VJP launch (K(X, X2): over the concatenation [X; X2]), and the kernel accumulates
+    its adjoint column sums in fp64 (sig_ho_bwd_lds.h); DESIGN.md 2.3, tools/diag_ho_grad.py."""
     import gpsig_amd
     from gpsig_amd import ops
     N, L, D, M = 2, 500, 24, 5
@@ -186,41 +192,22 @@ def test_higher_order_long_sequences_gradient(normalization):
     Xt.grad = None
     (k.K(Xt, X2t) * torch.as_tensor(G2, device=DEV)).sum().backward()
     gc, gc2 = Xt.grad.reshape(X.shape).cpu().numpy(), X2t.grad.reshape(X2.shape).cpu().numpy()
-    if not normalization:  # the normalised diagonal is the constant sum of the variances
-        Xt.grad = None
-        (k.Kdiag(Xt) * torch.as_tensor(Gd, device=DEV)).sum().backward()
-        gd = Xt.grad.reshape(X.shape).cpu().numpy()
 
     def ref(Y, Gm):
-        """fp64 gradients, and the scale the criterion is relative to: normalised, the gradient is the
-        small difference of the raw-level term and the diagonal terms (K_m is homogeneous of degree 2m in
-        the path, its normalisation scale-invariant), so the error is measured against the raw term alone
-        (the gradient with the normalising diagonals held fixed)"""
         Xr = torch.tensor(X, requires_grad=True)
         Yr = None if Y is None else torch.tensor(Y, requires_grad=True)
         (ar.K(Xr, Yr, M, base="linear", normalization=normalization, order=M) * torch.tensor(Gm)).sum().backward()
-        out = [Xr.grad.numpy()] + ([] if Y is None else [Yr.grad.numpy()])
-        if not normalization:
-            return out, [np.linalg.norm(o) for o in out]
-        Xs = torch.tensor(X, requires_grad=True)
-        Ys = None if Y is None else torch.tensor(Y, requires_grad=True)
-        Kl = ar.k_seq(Xs, Ys, M, "linear", order=M)
-        if Y is None:
-            dd = torch.sqrt(torch.diagonal(Kl, dim1=1, dim2=2).detach() + 1e-6)
-            den = dd[:, :, None] * dd[:, None, :]
-        else:
-            d1 = torch.sqrt(ar.k_seq_diag(Xs.detach(), M, "linear", order=M) + 1e-6)
-            d2 = torch.sqrt(ar.k_seq_diag(Ys.detach(), M, "linear", order=M) + 1e-6)
-            den = d1[:, :, None] * d2[:, None, :]
-        ((Kl / den).sum(0) * torch.tensor(Gm)).sum().backward()
-        return out, [np.linalg.norm(Xs.grad.numpy())] + ([] if Y is None else [np.linalg.norm(Ys.grad.numpy())])
+        return [Xr.grad.numpy()] + ([] if Y is None else [Yr.grad.numpy()])
 
-    (rs,), (ns,) = ref(None, G)
-    assert np.linalg.norm(gs - rs) < GTOL * ns
-    (rc, rc2), (nc, nc2) = ref(X2, G2)
-    assert np.linalg.norm(gc - rc) < GTOL * nc
-    assert np.linalg.norm(gc2 - rc2) < GTOL * nc2
+    (rs,) = ref(None, G)
+    assert norm_rel_err(gs, rs) < GTOL
+    rc, rc2 = ref(X2, G2)
+    assert norm_rel_err(gc, rc) < GTOL
+    assert norm_rel_err(gc2, rc2) < GTOL
     if not normalization:
+        Xt.grad = None  # the unnormalised diagonal (normalised it is the constant sum of the variances)
+        (k.Kdiag(Xt) * torch.as_tensor(Gd, device=DEV)).sum().backward()
+        gd = Xt.grad.reshape(X.shape).cpu().numpy()
         Xr = torch.tensor(X, requires_grad=True)
         (ar.k_seq_diag(Xr, M, "linear", True, order=M).sum(0) * torch.tensor(Gd)).sum().backward()
         assert norm_rel_err(gd, Xr.grad.numpy()) < GTOL

@@ -14,7 +14,7 @@ from conftest import norm_rel_err
 from oracle import autodiff_ref as ar
 
 pytestmark = pytest.mark.gpu
-GTOL = 5e-5
+GTOL = 1e-5
 DEV = "cuda"
 
 
