@@ -33,13 +33,17 @@ constexpr int MF_G = 4;                     // lane groups (x-sequences) per wav
 constexpr int MF_LP = 16;                   // lanes per pair (one DPP row)
 constexpr size_t MF_LDS_MAX = 160 * 1024;
 
-// K padding: KP = 4 KQ with KQ = 2 (mod 4), so the four K quarters of a 16x16x4 operand sit two banks
-// apart in the B image (conflict-free ds_read_b64) and every lane's A pair is 8-byte aligned.
+// K padding: KP = 4 KQ with KQ even (every lane's A pair 8-byte aligned): the MFMA loop runs KQ steps per K
+// quarter.  In the LDS B image the four quarters of a column sit QS apart, QS = KQ rounded up to 2 (mod 4), so
+// they are two banks apart (conflict-free ds_read_b64) without padding K itself (round 5: d = 46 ran KQ = 14,
+// 17 % more MFMA work than its KQ = 12; the bank stagger is now in the image's layout, not in K).
 __host__ __device__ inline int mf_kq(int d) {
   const int q = (d + 3) / 4;
-  return q + ((2 - q % 4) + 4) % 4;
+  return q + (q & 1);
 }
 __host__ __device__ inline int mf_kp(int d) { return 4 * mf_kq(d); }
+__host__ __device__ inline int mf_qs(int kq) { return kq + ((2 - kq % 4) + 4) % 4; }
+__host__ __device__ inline int mf_ldb(int d) { return 4 * mf_qs(mf_kq(d)) + 4; }
 // columns per lane by sequence length: one tile of LP W columns up to 160 points, past that W = 8 in column
 // blocks of LPW - 1 = 127 cells (the block's last column is the point of its first cell, below)
 __host__ __device__ inline int mf_w(int l) { return l <= 64 ? 4 : (l <= 128 ? 8 : (l <= 160 ? 10 : 8)); }
@@ -59,7 +63,7 @@ __host__ __device__ inline long long mf_rec_floats(int d, int l) {
 }
 inline size_t mf_lds_bytes(int d, int l2, int nw) {
   const size_t lpw = (size_t)mf_lpw(l2);
-  return (lpw * (size_t)(mf_kp(d) + 4) + (size_t)nw * 16 * (lpw + 4)) * sizeof(float);
+  return (lpw * (size_t)mf_ldb(d) + (size_t)nw * 16 * (lpw + 4)) * sizeof(float);
 }
 // waves per workgroup: 8 (two per SIMD, so one wave's matrix-core phase overlaps another's recursion) when
 // the LDS allows, else 4 (wide B images: d > 114 at 129..160 points); 0: no tile geometry
@@ -114,7 +118,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4)
   constexpr int CPB = LPW - 1;   // cells per column block
   const SigArgs &p = q.p;
   extern __shared__ __attribute__((aligned(16))) float mf_lds[];
-  const int KP = q.kp, KQ = KP / 4, LDB = KP + 4;
+  const int KP = q.kp, KQ = KP / 4, QS = mf_qs(KQ), LDB = 4 * QS + 4;
   float *__restrict__ Bs = mf_lds;
   const int lane = (int)threadIdx.x & 63;
   const int wave = wave_uniform((int)threadIdx.x >> 6);
@@ -140,13 +144,13 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4)
   const float *__restrict__ fyb = p.FY + (long long)b * q.ry;
   const float *__restrict__ pty = fyb + (long long)q.rowsy * KP;  // y's points
   // B image of column block j0: column jj < LPW - 1 = aug row j0 + jj + 1 (dy_{j0+jj}), column LPW - 1 = the
-  // point y_{j0}; k contiguous (stride LDB)
+  // point y_{j0}; column stride LDB, K quarter kq of a column at kq QS (k = kq KQ + r at kq QS + r)
   auto load_b = [&](int j0) {
-    const int k4n = KP / 4;
-    for (int e = (int)threadIdx.x; e < LPW * k4n; e += 64 * NW) {
-      const int j = e / k4n, k4 = e - j * k4n;
+    const int k2n = KP / 2;
+    for (int e = (int)threadIdx.x; e < LPW * k2n; e += 64 * NW) {
+      const int j = e / k2n, k = 2 * (e - j * k2n), kq = k / KQ;
       const float *src = j + 1 == LPW ? pty + (long long)j0 * KP : fyb + (long long)(j0 + j + 1) * KP;
-      *reinterpret_cast<f4 *>(Bs + j * LDB + 4 * k4) = *reinterpret_cast<const f4 *>(src + 4 * k4);
+      *reinterpret_cast<f2 *>(Bs + j * LDB + kq * QS + (k - kq * KQ)) = *reinterpret_cast<const f2 *>(src + k);
     }
   };
   load_b(0);
@@ -176,7 +180,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4)
     const int aa = tx * XB + wave * MF_G + (am >> 2);
     Asrc = p.FX + (long long)(aa < p.n1 ? aa : p.n1 - 1) * q.rx + (am & 3) * KP + (lane >> 4) * KQ;
   }
-  const float *__restrict__ Bl = Bs + (lane & 15) * LDB + (lane >> 4) * KQ;
+  const float *__restrict__ Bl = Bs + (lane & 15) * LDB + (lane >> 4) * QS;
   // the last tile column holds <dx_i, y_{j0}>: its writers subtract g_i there, so the tile carries p_{i,j0}
   const float *__restrict__ ggw;
   {
@@ -327,7 +331,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4)
       // lanes splitting the channels
       float s00 = 0.0f;
       for (int k = gl; k < q.d; k += LP) {
-        const float df = fx[k] - Bs[(LPW - 1) * LDB + k];
+        const float df = fx[k] - Bs[(LPW - 1) * LDB + (k / KQ) * QS + k % KQ];
         s00 = __builtin_fmaf(df, df, s00);
       }
       const float e00 = -0.5f * group_sum<LP>(s00);

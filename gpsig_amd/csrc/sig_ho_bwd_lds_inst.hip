@@ -1,6 +1,8 @@
 // gpsig_amd -- instantiations of the LDS-state higher-order Gram VJP (sig_ho_bwd_lds.h) for one effective
 // order (GPSIG_ORD): every level count whose multiplier slab fits the LDS, W = 4 (l2 <= 256) and 8 (l2 <= 512).
-#include "sig_ho_bwd_lds.h"
+#include <stdlib.h>
+
+#include "sig_ho_bwd_split.h"
 
 #ifndef GPSIG_ORD
 #error "GPSIG_ORD"
@@ -24,9 +26,35 @@ static int launch_lds(const BwdArgs &a, int seed, long long nblocks, hipStream_t
   }
 }
 
+// one pair over the 4 SIMDs of a CU (sig_ho_bwd_split.h): 257..509 points; GPSIG_HO_SPLIT=0 keeps the one-wave
+// kernel (A/B)
+template <int ORD, int M>
+static int launch_split(const BwdArgs &a, int seed, long long nblocks, hipStream_t s) {
+  constexpr size_t lds = ho_bwd_split_slab_bytes<ORD, M>();
+  if constexpr (lds + ho_bwd_lds_cbuf_bytes(8) + 2 * HO_SPLIT_NW * HO_SPLIT_XN * 4 > 160 * 1024) {
+    return GPSIG_EUNSUPPORTED;
+  } else {
+    if (seed == SEED_RBF_DIFF)
+      hipLaunchKernelGGL((sig_ho_bwd_split_kernel<ORD, M, SEED_RBF_DIFF>), dim3((unsigned)nblocks),
+                         dim3(64 * HO_SPLIT_NW), lds, s, a);
+    else if (seed == SEED_LIN_DIFF)
+      hipLaunchKernelGGL((sig_ho_bwd_split_kernel<ORD, M, SEED_LIN_DIFF>), dim3((unsigned)nblocks),
+                         dim3(64 * HO_SPLIT_NW), lds, s, a);
+    else
+      return GPSIG_EUNSUPPORTED;
+    return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
+  }
+}
+
+static bool split_on() {
+  const char *e = getenv("GPSIG_HO_SPLIT");
+  return !(e && e[0] == '0');
+}
+
 template <int ORD, int M>
 static int launch_lds_w(const BwdArgs &a, int seed, long long nblocks, hipStream_t s) {
   if (a.l2 <= 256) return launch_lds<ORD, M, 4>(a, seed, nblocks, s);
+  if (split_on() && ho_bwd_split_fits(ORD, M, a.l2)) return launch_split<ORD, M>(a, seed, nblocks, s);
   return launch_lds<ORD, M, 8>(a, seed, nblocks, s);
 }
 

@@ -24,6 +24,26 @@
 namespace gpsig {
 
 typedef float f4u __attribute__((ext_vector_type(4), aligned(4)));  // dword-aligned 16-byte loads
+typedef float f2u __attribute__((ext_vector_type(2), aligned(4)));  // dword-aligned 8-byte loads
+
+// W consecutive floats from q (dword-aligned): 16-byte loads, or 8-byte loads for W = 2 (the split higher-order
+// VJP, sig_ho_bwd_split.h)
+template <int W>
+GPSIG_DEV void ld_cols(const float *q, float (&v)[W]) {
+  if constexpr (W % 4 == 0) {
+#pragma unroll
+    for (int h = 0; h < W / 4; ++h) {
+      const f4u t = *reinterpret_cast<const f4u *>(q + 4 * h);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[4 * h + e] = t[e];
+    }
+  } else {
+    static_assert(W == 2, "columns per lane");
+    const f2u t = *reinterpret_cast<const f2u *>(q);
+    v[0] = t[0];
+    v[1] = t[1];
+  }
+}
 
 // Padded record length: every column a lane group reads (up to 512 past a column block's start) and
 // every row a chunk of R <= 8 rows reads stays inside the sequence's record; columns past the sequence
@@ -73,7 +93,7 @@ inline int diag_tile_pairs(const DiagTiles &dt, int n) {
 // slow rows) from another.
 template <int W, int R>
 struct RbfSeedWide {
-  static_assert(W == 4 || W == 8, "columns per lane");
+  static_assert(W == 2 || W == 4 || W == 8, "columns per lane");
   static constexpr int W2 = W / 2;
   static constexpr int ANCHOR = GPSIG_PK_ANCHOR;
   static constexpr float NHL2E = -0.72134752044448170f;
@@ -99,15 +119,7 @@ struct RbfSeedWide {
     f2 c[W2], p;
   };
 
-  GPSIG_DEV void lcols(const float *base, int k, float (&v)[W]) const {
-    const float *q = base + (long long)k * lw;
-#pragma unroll
-    for (int h = 0; h < W / 4; ++h) {
-      const f4u t = *reinterpret_cast<const f4u *>(q + 4 * h);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[4 * h + e] = t[e];
-    }
-  }
+  GPSIG_DEV void lcols(const float *base, int k, float (&v)[W]) const { ld_cols<W>(base + (long long)k * lw, v); }
 
   GPSIG_DEV void init(int d_, int lwx_, int lw_, const float *__restrict__ fxr, const float *__restrict__ fyblk, int gl,
                       int npts) {
@@ -185,15 +197,8 @@ struct RbfSeedWide {
   GPSIG_DEV void exact_tile(int t, f2 (&Eqo)[W2], f2 (&ko)[W2]) const {
     const float *kr = tke + (long long)(2 * t) * tld, *er = kr + tld;
     float kv[W], ev[W];
-#pragma unroll
-    for (int h = 0; h < W / 4; ++h) {
-      const f4u a = *reinterpret_cast<const f4u *>(kr + 4 * h), b = *reinterpret_cast<const f4u *>(er + 4 * h);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        kv[4 * h + e] = a[e];
-        ev[4 * h + e] = b[e];
-      }
-    }
+    ld_cols<W>(kr, kv);
+    ld_cols<W>(er, ev);
 #pragma unroll
     for (int w2 = 0; w2 < W2; ++w2) {
       ko[w2] = (f2){kv[w2], kv[w2 + W2]};
@@ -208,12 +213,7 @@ struct RbfSeedWide {
     for (int r = 0; r < R; ++r) {
       const float *cr = tcc + (long long)(i0 + r) * tld, *pr = tpp + (long long)(i0 + r) * tld;
       float cv[W];
-#pragma unroll
-      for (int h = 0; h < W / 4; ++h) {
-        const f4u a = *reinterpret_cast<const f4u *>(cr + 4 * h);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) cv[4 * h + e] = a[e];
-      }
+      ld_cols<W>(cr, cv);
       cv[W - 1] *= mlast;
 #pragma unroll
       for (int w2 = 0; w2 < W2; ++w2) cc[r][w2] = (f2){cv[w2], cv[w2 + W2]};
@@ -362,15 +362,7 @@ struct WideSeedGen {
     f2 c[W2];
   };
 
-  GPSIG_DEV void lcols(const float *base, int k, float (&v)[W]) const {
-    const float *q = base + (long long)k * lw;
-#pragma unroll
-    for (int h = 0; h < W / 4; ++h) {
-      const f4u t = *reinterpret_cast<const f4u *>(q + 4 * h);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) v[4 * h + e] = t[e];
-    }
-  }
+  GPSIG_DEV void lcols(const float *base, int k, float (&v)[W]) const { ld_cols<W>(base + (long long)k * lw, v); }
 
   GPSIG_DEV void init(int d_, int lwx_, int lw_, const float *__restrict__ fxr, const float *__restrict__ fyblk, int gl,
                       int npts) {

@@ -327,10 +327,10 @@ def test_tens_vs_seq_vjp_matches_autodiff(base, increments, M, D, L):
 
 @pytest.mark.parametrize("base", ["rbf", "linear"])
 @pytest.mark.parametrize("increments", [False, True])
-@pytest.mark.parametrize("D", [3, 46])
+@pytest.mark.parametrize("D", [3, 46, 126])
 def test_tens_gram_vjp_matches_autodiff(base, increments, D):
-    """K_tens (Kzz, summed over levels x sigma*variances) gradients in Z and lengthscales (D = 46: the
-    pair-tile + GEMM path, csrc/tens_vjp_mm.hip)."""
+    """K_tens (Kzz, summed over levels x sigma*variances) gradients in Z and lengthscales (D = 46 and 126, the
+    CMU runners' channel count after lag and time: the pair-tile + GEMM path, csrc/tens_vjp_mm.hip)."""
     import gpsig_amd
     M, T = 4, 70
     LT = M * (M + 1) // 2

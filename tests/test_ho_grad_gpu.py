@@ -95,6 +95,8 @@ def _walks(n, l, d, seed):
     # the LDS-state kernel (csrc/sig_ho_bwd_lds.h): orders 4-5, order 3 past 5 levels, 257-512 points
     (25, 3, 5, 4, "rbf"), (20, 2, 5, 5, "linear"), (22, 3, 6, 3, "rbf"), (16, 2, 7, 5, "rbf"),
     (19, 4, 4, 4, "linear"), (300, 3, 4, 2, "rbf"), (270, 2, 5, 5, "linear"), (400, 3, 5, 4, "rbf"),
+    # 257-509 points: one pair over the 4 SIMDs of a CU (csrc/sig_ho_bwd_split.h), 3 and 4 column blocks
+    (381, 3, 4, 3, "rbf"), (509, 2, 3, 2, "linear"),
 ])
 def test_higher_order_vjp_kernel_raw_levels(L, D, M, order, base):
     """gpsig_sig_gram_vjp_ho (csrc/sig_ho_bwd.h, sig_ho_bwd_lds.h) against fp64 autodiff of
@@ -263,3 +265,32 @@ def test_higher_order_vjp_chunked_upper_vs_rect():
     gS, _ = ops.sig_gram_vjp(Xt, None, M, Gt, base="rbf", gout_levels=True, order=order)
     gX, gY = ops.sig_gram_vjp(Xt, Xt.clone(), M, Gt, base="rbf", gout_levels=True, order=order)
     assert norm_rel_err(gS.cpu().numpy(), (gX + gY).cpu().numpy()) < 1e-5
+
+
+@pytest.mark.parametrize("L,M,order,base", [(300, 4, 2, "rbf"), (500, 5, 5, "linear"), (390, 3, 3, "rbf")])
+def test_higher_order_vjp_split_matches_one_wave_kernel(L, M, order, base, monkeypatch):
+    """The 4-wave split of the LDS-state VJP (sig_ho_bwd_split.h) against the one-wave kernel it replaces
+    (GPSIG_HO_SPLIT=0): the same recursion with the column scans combined across blocks, so the gradients
+    agree to fp32 rounding of the scans; UPPER, RECT and DIAG pairs."""
+    from gpsig_amd import ops
+    D = 5
+    X, Y = _walks(3, L, D, L + 1), _walks(2, L - 7, D, L + 2)
+    G = np.random.default_rng(17).standard_normal((M + 1, 3, 2))
+    Gs = np.random.default_rng(18).standard_normal((M + 1, 3, 3))
+    Gd = np.random.default_rng(19).standard_normal((M + 1, 3))
+    Xt, Yt = torch.tensor(X, device=DEV, dtype=torch.float32), torch.tensor(Y, device=DEV, dtype=torch.float32)
+
+    def grads():
+        out = list(ops.sig_gram_vjp(Xt, Yt, M, torch.tensor(G, device=DEV), base=base, gout_levels=True,
+                                    order=order))
+        out.append(ops.sig_gram_vjp(Xt, None, M, torch.tensor(Gs, device=DEV), base=base, gout_levels=True,
+                                    order=order)[0])
+        out.append(ops.sig_gram_vjp(Xt, None, M, torch.tensor(Gd, device=DEV), base=base, diag=True,
+                                    order=order)[0])
+        return [g.cpu().numpy() for g in out]
+
+    split = grads()
+    monkeypatch.setenv("GPSIG_HO_SPLIT", "0")
+    one = grads()
+    for g, r in zip(split, one):
+        assert norm_rel_err(g, r) < 2e-6

@@ -218,7 +218,42 @@ def bench_svgp(reps, t=500, n=50, l=500, nf=23, m=4):
         v.requires_grad_(False)
     return dict(path=f"svgp_d{D}", workload=f"SVGP step Kuu_Kuf_Kff SignatureRBF num_levels={m} num_lags=1 D={D} "
                 f"InducingTensors T={t} increments=True, minibatch N={n} L={l} (dZ, dlengthscales, dvariances)",
-                fwd_ms=tf * 1e3, fwd_bwd_ms=tb * 1e3, grad_err=None)
+                fwd_ms=tf * 1e3, fwd_bwd_ms=tb * 1e3, grad_err=svgp_grad_err(Xnp, Z0, nf, m))
+
+
+def svgp_grad_err(Xnp, Z0, nf, m, ts=16, ns=2):
+    """The same bundle's gradients on a subsample (the first ts inducing tensors, ns sequences, full length
+    and channel count) against fp64 autodiff of the reference graph: Kzz = tensor_kern x sigma*variances,
+    Kzx normalised by the sequences' diagonals (kernels.py:624-704), the scaling and lags (kernels.py:344-399)
+    restated by the kernel's own torch code on CPU float64.  Max over dZ, dlengthscales, dvariances of
+    max|g - g64| / max|g64|."""
+    import gpsig_amd
+    from gpsig_amd.inducing_variables import InducingTensors
+    from oracle import autodiff_ref as ar
+    l = Xnp.shape[1]
+    Z = Z0[:, :ts].detach().cpu().numpy()
+    X = Xnp[:ns]
+    rng = np.random.default_rng(9)
+    Gzz, Gzx = rng.standard_normal((ts, ts)), rng.standard_normal((ts, ns))
+    out = {}
+    for dev in ("cuda", "cpu"):
+        k = gpsig_amd.SignatureRBF(l * nf, nf, m, num_lags=1, lengthscales=np.ones(nf))
+        k.to(dev)
+        for v in (k.lengthscales, k.variances):
+            v.requires_grad_(True)
+        Zt = torch.tensor(Z, device=dev, requires_grad=True)
+        Xt = torch.tensor(X.reshape(ns, -1), device=dev)
+        if dev == "cuda":
+            Kzz, Kzx, _ = InducingTensors(Zt, m, increments=True).Kuu_Kuf_Kff(k, Xt)
+        else:  # fp64 reference graph on the kernel's own scaling of the same parameters
+            Xs = k._prep(Xt)
+            Zs = k._apply_scaling_to_incremental_tensors(Zt)
+            sv = k.sigma * k.variances
+            Kzz = (ar.k_tens(Zs, m, "rbf", increments=True) * sv[:, None, None]).sum(0)
+            Kzx = ar.K_tens_vs_seq(Zs, Xs, m, base="rbf", increments=True, scale=sv)
+        ((Kzz * torch.tensor(Gzz, device=dev)).sum() + (Kzx * torch.tensor(Gzx, device=dev)).sum()).backward()
+        out[dev] = [t.grad.detach().cpu().double().numpy() for t in (Zt, k.lengthscales, k.variances)]
+    return max(rel(g, r) for g, r in zip(out["cuda"], out["cpu"]))
 
 
 def bench_vosf_kdiag(reps, n=50, l=500, nf=23, m=5):
