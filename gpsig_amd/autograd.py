@@ -23,7 +23,9 @@ its diagonal through gpsig_sig_gram_vjp_ho (csrc/sig_ho_bwd.h, sig_ho_bwd_lds.h:
 lengths <= 512, where the row state fits the LDS)
 and, beyond it, for SignatureLinear with order >= num_levels (the exact signature kernel; backward
 through the signature features, ops.sig_gram_ho_vjp); other higher orders evaluate forward but raise
-NotImplementedError on backward.
+NotImplementedError on backward.  The RBF higher order past 32 channels takes its cells from the matrix-core
+producer, whose LDS image of one sequence bounds d to about 180 channels at 129-160 points and about 240
+otherwise (include/gpsig_amd.h, gpsig_sig_workspace_bytes_ex): past that the forward raises GpsigError.
 """
 from __future__ import annotations
 
@@ -141,11 +143,15 @@ def _epilogue(Kr, sc, cfg):
     return K if cfg["return_levels"] else K.sum(0)
 
 
-def _ho_folded(cfg, needs_grad):
-    """Higher-order normalised K under the higher-order VJP kernel: the forward keeps the raw levels (and, for
-    K(X, X2), the raw diagonals) and the backward folds the normalisation's diagonal terms into the weights of
-    the diagonal pairs (one VJP launch, see SigGram.backward)."""
-    return needs_grad and cfg["normalization"] and cfg["order"] > 1 and cfg["num_levels"] > 1
+def _folded(cfg, X2s, lengths, needs_grad):
+    """Normalised K whose backward folds the normalisation's diagonal terms into the weights of the diagonal
+    pairs (one VJP launch, see SigGram.backward): the forward keeps the raw levels (and, for K(X, X2), the raw
+    diagonals).  Order 1: symmetric K(X); higher orders: under the higher-order VJP kernel, K(X) and K(X, X2)."""
+    if not (needs_grad and cfg["normalization"] and cfg["num_levels"] > 1):
+        return False
+    if cfg["order"] == 1:
+        return X2s is None
+    return _ho_vjp_kernel(cfg, *lengths)
 
 
 def _epilogue_cross(Kr, d1, d2, sc, cfg):
@@ -176,14 +182,18 @@ class SigGram(torch.autograd.Function):
     def forward(ctx, Xs, X2s, scale, cfg):
         M = cfg["num_levels"]
         lengths = (Xs.shape[1],) if X2s is None else (max(Xs.shape[1], X2s.shape[1]),)
-        if _ho_folded(cfg, any(ctx.needs_input_grad[:3])) and _ho_vjp_kernel(cfg, *lengths):
+        if _folded(cfg, X2s, lengths, any(ctx.needs_input_grad[:3])):
             # raw levels (and diagonals) from the kernels, the epilogue in fp64 (the backward differentiates it)
             kw = dict(order=cfg["order"], base=cfg["base"], difference=cfg["difference"])
-            Kr = ops.sig_gram(Xs.detach(), None if X2s is None else X2s.detach(), M, **kw)
+            state = None
+            if cfg["order"] == 1 and cfg["difference"]:  # the VJP then skips its forward sweep
+                numel = ops.sig_state_numel(Xs.shape[0], None, Xs.shape[1], M)
+                state = _saved_buffer(numel, Xs.device, GRAM_STATE_BYTES)
+            Kr = ops.sig_gram(Xs.detach(), None if X2s is None else X2s.detach(), M, state=state, **kw)
             sc32 = scale.detach().to(torch.float32)
             ctx.cfg = cfg
             ctx.scale_dtype = scale.dtype
-            ctx.state = None
+            ctx.state = state
             ctx.folded = True
             if X2s is None:
                 ctx.save_for_backward(Xs, X2s, sc32, Kr, None, None)
@@ -219,10 +229,10 @@ class SigGram(torch.autograd.Function):
         cfg = ctx.cfg
         if ctx.folded:
             # dLoss/dK_m(a, b) of the epilogue in fp64, the diagonal's own term (through 1/sqrt(K_m(a, a)))
-            # included in the weight of the pair (a, a): ONE VJP launch over the upper triangle, whose two
-            # emission sides are summed in fp64 (sig_bwd_wide.hip).  Computed as separate Gram and diagonal
-            # VJPs, the two terms cancel ~270x at the VOSF trainer's shape and their fp32
-            # rounding dominated the gradient.
+            # included in the weight of the pair (a, a): ONE VJP launch over the upper triangle.  The diagonal
+            # term's direction is the pair (a, a)'s own derivative, so its large part cancels in the scalar
+            # weight; computed as separate Gram and diagonal VJPs the two terms cancel ~270x at the VOSF
+            # trainer's shape and their fp32 rounding dominated the gradient.
             Xs, X2s, sc32, Kr, d1, d2 = ctx.saved_tensors
             vjp = dict(base=cfg["base"], gout_levels=True, difference=cfg["difference"], order=cfg["order"])
             M = cfg["num_levels"]
@@ -231,7 +241,8 @@ class SigGram(torch.autograd.Function):
                     K64 = Kr.double().requires_grad_(True)
                     sc = sc32.double().requires_grad_(True)
                     gK, gsc = torch.autograd.grad(_epilogue(K64, sc, cfg), [K64, sc], gout.double())
-                gX, _ = ops.sig_gram_vjp(Xs.detach(), None, M, gK.to(torch.float32), **vjp)
+                gX, _ = ops.sig_gram_vjp(Xs.detach(), None, M, gK.to(torch.float32), state=ctx.state, **vjp)
+                ctx.state = None
                 return (gX.to(Xs.dtype) if ctx.needs_input_grad[0] else None, None,
                         gsc.to(ctx.scale_dtype) if ctx.needs_input_grad[2] else None, None)
             # K(X, X2): the Gram pairs and both sets of diagonal pairs in ONE upper-triangle launch over the

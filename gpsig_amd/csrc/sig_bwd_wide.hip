@@ -92,6 +92,7 @@ int wide_diag_tiles(const float *FX, long long sx, int d, int lw, int a0, int np
                            hipStream_t s) {
   const float *rec = FX + (long long)a0 * sx;
   int rc;
+  if (npairs > 65535) return GPSIG_EUNSUPPORTED;  // the anchor launch's grid z; checked before any launch
   // c_ij: op(A)[i][k] = dx_k[i], op(B)[k][j] = dx_k[j]
   if ((rc = gemm_f32(s, true, false, (int)dt.rows, (int)dt.ld, d, 1.0f, rec + (long long)d * lw, lw, sx,
                      rec + (long long)d * lw, lw, sx, 0.0f, T, dt.ld, dt.pair, npairs, 0, 0, nullptr, 0)))
@@ -101,7 +102,6 @@ int wide_diag_tiles(const float *FX, long long sx, int d, int lw, int a0, int np
                      0.0f, T + dt.rows * dt.ld, dt.ld, dt.pair, npairs, 0, 0, nullptr, 0)))
     return rc;
   const long long na = dt.rows / DIAG_TILE_ANCHOR;
-  if (npairs > 65535) return GPSIG_EUNSUPPORTED;
   hipLaunchKernelGGL(wide_diag_anchor_kernel,
                      dim3((unsigned)((dt.ld + 255) / 256), (unsigned)((na + ANCHOR_G - 1) / ANCHOR_G), (unsigned)npairs),
                      dim3(256), 0, s, rec, sx, d, lw, dt, T);

@@ -14,6 +14,8 @@
 // column is the halo point), left to right over all rows; the exclusive column scans of a block add the
 // carry of the blocks to its left: per row, one float per scanned quantity (S00 and Sa[1..dn-1] of each
 // level), kept in this wave's LDS slab.
+#include <stdlib.h>
+
 #include "sig_common.h"
 #include "gemm.h"
 
@@ -66,7 +68,13 @@ GPSIG_DEV void excl_scan_cols(const float (&v)[W], float (&out)[W], float *cr, i
 // TILE (linear base kernel, any channel count): the cells come from the increment-Gram tile of the
 // launch (SigArgs::tile, a GEMM of the increments, the reference's own tf.matmul of the linear base
 // kernel, kernels.py:1042-1044), DP is unused.
-template <int DP, int W, int ORD, int MMAX, int SEED, bool TILE = false>
+// SPLIT (round 5): one pair per workgroup, its column blocks (2..4) side by side on the 4 waves instead of one
+// after another on one wave: every exclusive column scan of a row adds the totals of the blocks to its left,
+// exchanged through LDS, one barrier per level and row (the scans of a level at once).  For calls with few
+// pairs (the VOSF trainer's Kff diagonal: 50 pairs of 500 points = 50 waves) it puts 4 SIMDs on each pair.
+// The workgroups enumerate the pairs in the order of the 4-pair workgroups of the plain kernel (slot =
+// blockIdx.x & 3), so the launches share the host's pair counts (x 4).
+template <int DP, int W, int ORD, int MMAX, int SEED, bool TILE = false, bool SPLIT = false>
 __global__ __launch_bounds__(256) void sig_ho_kernel(SigArgs p) {
   using Seed = RowSeed<DP, W, SEED>;
   using Lay = HoLayout<ORD, MMAX>;
@@ -74,29 +82,34 @@ __global__ __launch_bounds__(256) void sig_ho_kernel(SigArgs p) {
   static_assert(!TILE || SEED == SEED_LIN_DIFF, "tile cells: linear difference seed");
   const int lane = threadIdx.x & 63;
   const int wave = wave_uniform(threadIdx.x >> 6);
+  const int slot = SPLIT ? (int)(blockIdx.x & 3) : wave;                   // the pair's slot in its group of 4
+  const long long grp = SPLIT ? (long long)(blockIdx.x >> 2) : (long long)blockIdx.x;
 
   int a, b;
   if (p.pair_mode == GPSIG_PAIRS_DIAG) {
-    a = p.row_begin + (int)blockIdx.x * 4 + wave;
+    a = p.row_begin + (int)grp * 4 + slot;
     b = a;
     if (a >= p.row_end) return;
   } else {
     int ta, tb;
     if (p.pair_mode == GPSIG_PAIRS_UPPER) {
-      const Tile t = upper_tile(p.tile_base + (long long)blockIdx.x, p.ntb, 4);
+      const Tile t = upper_tile(p.tile_base + grp, p.ntb, 4);
       ta = t.ta;
       tb = t.tb;
     } else {
-      ta = p.tiles_a0 + (int)blockIdx.x / p.ntb;
-      tb = (int)blockIdx.x % p.ntb;
+      ta = p.tiles_a0 + (int)(grp / p.ntb);
+      tb = (int)(grp % p.ntb);
     }
-    a = ta * 4 + wave;
+    a = ta * 4 + slot;
     b = tb;
     if (a < p.row_begin || a >= p.row_end) return;
   }
   bool pair_ok = b < p.n2;
   if (p.pair_mode == GPSIG_PAIRS_UPPER) pair_ok = pair_ok && b >= a;
-  if (!pair_ok) return;  // one pair per wave: wave-uniform
+  if (!pair_ok) return;  // one pair per wave (SPLIT: per workgroup): uniform
+  // SPLIT: per-wave totals of the current exchange (double-buffered), the pair's level sums at the end
+  __shared__ float hx[SPLIT ? 2 : 1][SPLIT ? 4 : 1][SPLIT ? ORD : 1];
+  int ph = 0;
 
   const float *__restrict__ fx = TILE ? nullptr : p.FX + (long long)a * p.l1 * FS;
   const float *__restrict__ fy = TILE ? nullptr : p.FY + (long long)b * p.l2 * FS;
@@ -116,14 +129,16 @@ __global__ __launch_bounds__(256) void sig_ho_kernel(SigArgs p) {
 #pragma unroll
   for (int m = 0; m <= MMAX; ++m) Kacc[m] = 0.0f;
 
-  for (int blk = 0; blk < nblk; ++blk) {
-  const int j0 = blk * CPB;
+  for (int blk = SPLIT ? wave : 0; blk < (SPLIT ? wave + 1 : nblk); ++blk) {
+  // SPLIT: a wave past the last block keeps a valid record view (block 0) and contributes zero cells
+  const bool idle = SPLIT && blk >= nblk;
+  const int j0 = idle ? 0 : blk * CPB;
   Seed seed;
   if constexpr (!TILE) seed.init(fx, fy + (long long)j0 * FS, lane, nblk == 1 ? p.l2 : min(p.l2 - j0, CPB + 1));
   // TILE: this lane's cell columns of the block (the halo column of a block is not a cell of it)
   bool tcol[W];
 #pragma unroll
-  for (int w = 0; w < W; ++w) tcol[w] = lane * W + w < CPB && j0 + lane * W + w < p.l2 - 1;
+  for (int w = 0; w < W; ++w) tcol[w] = !idle && lane * W + w < CPB && j0 + lane * W + w < p.l2 - 1;
 
   float CB[Lay::total][W];
 #pragma unroll
@@ -144,6 +159,9 @@ __global__ __launch_bounds__(256) void sig_ho_kernel(SigArgs p) {
     } else {
       rn.load(fx, i + 1 < nrows ? i + 1 : i, SEED);
       seed.template row<true>(rd, dM);
+      if (idle)
+#pragma unroll
+        for (int w = 0; w < W; ++w) dM[w] = 0.0f;
     }
 
     float R[ORD][ORD][W];
@@ -185,11 +203,48 @@ __global__ __launch_bounds__(256) void sig_ho_kernel(SigArgs p) {
               if (x < dmv) s += CB[Lay::off(m) + x][w];
             tot[w] = s;
           }
-          excl_scan_cols<W>(tot, S00, cr + Lay::coff(m), blk, nblk);
           float Sa[ORD][W];
+          if constexpr (SPLIT) {
+            // the dn scans of the level together: in-lane and over the wave, then the blocks to the left
+            float in[ORD][W], t[ORD], incl[ORD];
 #pragma unroll
-          for (int x = 1; x < ORD; ++x)
-            if (x < dn) excl_scan_cols<W>(rowsum[x - 1], Sa[x], cr + Lay::coff(m) + x, blk, nblk);
+            for (int x = 0; x < ORD; ++x)
+              if (x < dn)
+#pragma unroll
+                for (int w = 0; w < W; ++w) in[x][w] = x == 0 ? tot[w] : rowsum[x - 1][w];
+#pragma unroll
+            for (int x = 0; x < ORD; ++x)
+              if (x < dn) {
+                float c = 0.0f;
+#pragma unroll
+                for (int w = 0; w < W; ++w) c += in[x][w];
+                t[x] = c;
+                incl[x] = group_incl_scan<64>(c);
+              }
+            if (lane == 63)
+#pragma unroll
+              for (int x = 0; x < ORD; ++x)
+                if (x < dn) hx[ph][wave][x] = incl[x];
+            __syncthreads();
+#pragma unroll
+            for (int x = 0; x < ORD; ++x)
+              if (x < dn) {
+                float base = incl[x] - t[x];
+#pragma unroll
+                for (int u = 0; u < 4; ++u)
+                  if (u < wave) base += hx[ph][u][x];
+                float *o = x == 0 ? S00 : Sa[x];
+                o[0] = base;
+#pragma unroll
+                for (int w = 1; w < W; ++w) o[w] = o[w - 1] + in[x][w - 1];
+              }
+            ph ^= 1;
+          } else {
+            excl_scan_cols<W>(tot, S00, cr + Lay::coff(m), blk, nblk);
+#pragma unroll
+            for (int x = 1; x < ORD; ++x)
+              if (x < dn) excl_scan_cols<W>(rowsum[x - 1], Sa[x], cr + Lay::coff(m) + x, blk, nblk);
+          }
           // new blocks, in place: same-cell chain first (descending), then the edges
 #pragma unroll
           for (int x = ORD - 1; x >= 1; --x)
@@ -243,6 +298,16 @@ __global__ __launch_bounds__(256) void sig_ho_kernel(SigArgs p) {
   K[0] = 1.0f;
 #pragma unroll
   for (int m = 1; m <= MMAX; ++m) K[m] = Kacc[m];
+  if constexpr (SPLIT) {  // the blocks' level sums (every wave holds its block's in every lane)
+    __shared__ float ks[4][MMAX + 1];
+    if (lane == 0)
+#pragma unroll
+      for (int m = 1; m <= MMAX; ++m) ks[wave][m] = Kacc[m];
+    __syncthreads();
+#pragma unroll
+    for (int m = 1; m <= MMAX; ++m) K[m] = ((ks[0][m] + ks[1][m]) + ks[2][m]) + ks[3][m];
+    if (wave != 0) return;
+  }
   if constexpr (TILE) {
     // level 1 in closed form (fp64, channels over the lanes): linear sum_ij <dx_i, dy_j> = <x_L - x_0, y_L - y_0>,
     // RBF cells (tile_rbf) the corner difference k(x_L, y_L) - k(x_L, y_0) - k(x_0, y_L) + k(x_0, y_0)
@@ -288,11 +353,24 @@ static size_t ho_carry_bytes(int l1, int order, int M, int nblk) {
 }
 constexpr size_t HO_MAX_CARRY_BYTES = 160 * 1024;
 
+// the split form (one pair per workgroup, column blocks side by side) for calls with few pairs: below about
+// two waves per SIMD the plain kernel leaves the chip idle (GPSIG_HO_SPLIT=0 keeps the plain kernel)
+constexpr long long HO_SPLIT_PAIRS = 2048;
+static bool ho_split_on() {
+  const char *e = getenv("GPSIG_HO_SPLIT");
+  return !(e && e[0] == '0');
+}
+
 template <int DP, int W, int ORD, int SEED, bool TILE = false>
 static int launch_ho(const SigArgs &a0, long long nblocks, hipStream_t s) {
   if (nblocks <= 0) return GPSIG_OK;
   SigArgs a = a0;
   a.nblk = ho_blocks(a.l2, W);
+  if (a.nblk >= 2 && a.nblk <= 4 && nblocks * 4 <= HO_SPLIT_PAIRS && ho_split_on()) {
+    hipLaunchKernelGGL((sig_ho_kernel<DP, W, ORD, 8, SEED, TILE, true>), dim3((unsigned)(nblocks * 4)), dim3(256), 0,
+                       s, a);
+    return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
+  }
   const size_t lds = ho_carry_bytes(a.l1, ORD, a.M, a.nblk);
   if (lds > HO_MAX_CARRY_BYTES) return GPSIG_EUNSUPPORTED;
   hipLaunchKernelGGL((sig_ho_kernel<DP, W, ORD, 8, SEED, TILE>), dim3((unsigned)nblocks), dim3(256), lds, s, a);

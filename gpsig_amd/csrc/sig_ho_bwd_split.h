@@ -108,7 +108,7 @@ __global__ __launch_bounds__(64 * HO_SPLIT_NW) __attribute__((amdgpu_waves_per_e
   for (int w = 0; w < W; ++w) {
     const int jj = lane * W + w;
     colv[w] = jj < CPB && j0 + jj < l2 - 1;
-    ptv[w] = jj < CPB && j0 + jj < l2;
+    ptv[w] = j0 + jj < l2 && (jj < CPB || wave == NW - 1);  // a block's halo point is the next block's first
   }
 
   // cross-block exchange: N per-wave values (uniform in the wave) -> every wave's values; one barrier

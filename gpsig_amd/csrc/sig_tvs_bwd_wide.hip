@@ -181,9 +181,10 @@ __device__ __forceinline__ void tvsw_level(const TvsBwdWideArgs &a) {
     for (int c = 0; c < I; ++c) m[c] = RBF ? (INCR ? v1[c] - v0[c] : v0[c]) : v0[c];
   };
   // k(z0, x) carried along the sweep by e^{+-q} (sgn q: the exponent of this step), re-evaluated exactly every
-  // ANCHOR points, wherever the step factor leaves [e^-20, e^20], and wherever a carried value below 1e-30 is
-  // about to grow: once it has underflowed to 0 (or a denormal) the product cannot bring it back, while the
-  // exact value may have climbed to O(1) by the next anchor (wave-uniform)
+  // ANCHOR points, wherever |q| >= 2 (the rounding of q costs |q| eps of the exponent per carried step: the
+  // forward kernel's TVS_CORNER), and wherever a carried value below 1e-30 is about to grow: once it has
+  // underflowed to 0 (or a denormal) the product cannot bring it back, while the exact value may have climbed
+  // to O(1) by the next anchor (wave-uniform)
   auto far = [](const float (&qv)[I], const float (&kv)[I], float sgn) {
     float mx = 0.f;
     bool tiny = false;
@@ -192,7 +193,7 @@ __device__ __forceinline__ void tvsw_level(const TvsBwdWideArgs &a) {
       mx = __builtin_fmaxf(mx, __builtin_fabsf(qv[c]));
       tiny = tiny || (kv[c] < 1e-30f && sgn * qv[c] > 0.f);
     }
-    return __builtin_amdgcn_ballot_w64(mx > 20.0f || tiny) != 0;
+    return __builtin_amdgcn_ballot_w64(mx >= 2.0f || tiny) != 0;
   };
 
   const float gI = valid ? a.gout[((long long)I * T + tt) * n + sq] : 0.f;
@@ -447,8 +448,8 @@ static TvswPlan tvsw_plan(int n, int l, int d, int lt, int t, bool incr) {
   TvswPlan p{};
   // a chunk's tiles: the weights (W0, W1) and the seeds (SD, SX with H = 2), ~6 (lt t l) floats per sequence
   long long nc = (long long)(tvs_tile_budget() / ((size_t)lt * t * l * sizeof(float) * 6));
-  nc = nc < 64 ? 64 : (nc / 64) * 64;
-  if (nc > ((n + 63) / 64) * 64) nc = ((n + 63) / 64) * 64;
+  nc = nc < 64 ? 64 : (nc / 64) * 64;  // whole waves of sequences per chunk, or all of them in one
+  if (nc > n) nc = n;
   p.nc = (int)nc;
   p.ft = a256(tvs_features_bytes(n, l, d));
   p.zw = a256((size_t)t * tvsw_zs(d, lt, true) * sizeof(float));

@@ -364,8 +364,8 @@ inline TvsSeedPlan tvs_seed_plan(int n, int l, int d, int lt, int t) {
   TvsSeedPlan p{};
   const size_t per_seq = (size_t)(l - 1) * t * lt * 2 * sizeof(float);  // H = 2: the largest tile
   long long nc = per_seq ? (long long)(tvs_tile_budget() / per_seq) : n;
-  nc = nc < 64 ? 64 : (nc / 64) * 64;
-  if (nc > ((n + 63) / 64) * 64) nc = ((n + 63) / 64) * 64;
+  nc = nc < 64 ? 64 : (nc / 64) * 64;  // whole waves of sequences per chunk ...
+  if (nc > n) nc = n;                   // ... or every sequence in one chunk (fewer than 64 only then)
   p.nc = (int)nc;
   p.a = (((size_t)t * lt * 2 * d * sizeof(float)) + 255) & ~(size_t)255;
   p.dx = (((size_t)nc * (l - 1) * d * sizeof(float)) + 255) & ~(size_t)255;

@@ -84,6 +84,7 @@ constexpr size_t DIAG_TILE_BYTES = (size_t)512 << 20;
 inline int diag_tile_pairs(const DiagTiles &dt, int n) {
   long long p = (long long)(DIAG_TILE_BYTES / ((size_t)dt.pair * sizeof(float)));
   if (p < 4) p = 4;
+  if (p > 65535) p = 65535;  // the anchor launch's grid z (wide_diag_tiles)
   return (int)(p < n ? p : n);
 }
 

@@ -89,9 +89,12 @@ enum gpsig_out_mode {
  */
 size_t gpsig_sig_workspace_bytes(int n1, int l1, int n2, int l2, int d);
 /* The workspace of one gpsig_sig_gram / gpsig_sig_diag call given its order and pair mode: as above,
- * except the higher-order recursion past 32 channels (linear base kernel only), whose cells come from
- * an increment-Gram tile -- the reference's tf.matmul of the linear base kernel (kernels.py:1042-1044) --
- * built by a matrix-core GEMM per chunk of x-rows: the increments plus one chunk's tile (<= 1 GiB). */
+ * except the higher-order recursion past 32 channels, whose cells come from a tile -- for the linear base
+ * kernel the reference's tf.matmul (kernels.py:1042-1044), a matrix-core GEMM per chunk of x-rows; for the
+ * RBF base kernel the matrix-core cell producer of the wide first-order Gram -- the increments plus one
+ * chunk's tile (<= 1 GiB).  Channel bound of the RBF higher order past 32 channels: the producer keeps one
+ * y-sequence's increments in LDS (160 KiB), which holds d up to about 180 channels at 129-160 points and
+ * about 240 otherwise; past that the call returns GPSIG_EUNSUPPORTED (the linear kernel has no bound). */
 size_t gpsig_sig_workspace_bytes_ex(int n1, int l1, int n2, int l2, int d, int order, int pair_mode);
 /* Extra workspace of a GPSIG_GRAM_SPLIT call (one chunk of pairs' cells); 0 where the split does not apply. */
 size_t gpsig_sig_split_bytes(int l1, int l2, int d, int num_levels);

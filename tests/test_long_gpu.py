@@ -141,3 +141,30 @@ def test_long_pde_kernel_class_kdiag():
     got = k.Kdiag(t(X.reshape(4, -1))).cpu().numpy()
     exp = pde.pde_diag(X, 2, 1)
     assert np.abs(got - exp).max() / np.abs(exp).max() < TOL
+
+
+@pytest.mark.parametrize("L,M,order,base", [(200, 5, 5, "linear"), (500, 5, 5, "linear"), (300, 4, 3, "rbf"),
+                                            (260, 6, 2, "rbf")])
+def test_higher_order_split_forward_matches_plain(L, M, order, base, monkeypatch):
+    """The split higher-order forward (sig_ho.hip SPLIT: one pair per workgroup, column blocks side by side on
+    the 4 waves, the block carries exchanged through LDS) against the plain kernel (column blocks one after
+    another on one wave, GPSIG_HO_SPLIT=0): the same cells and recursion, the column scans combined in another
+    order, so the levels agree to fp32 rounding; K(X, Y), K(X) and the diagonal."""
+    from gpsig_amd import ops
+    D = 24 if base == "linear" else 4  # linear order >= M at few channels runs as signature features instead
+    rng = np.random.default_rng(L + M)
+    X = np.cumsum(rng.standard_normal((3, L, D)), 1) / np.sqrt(L * D)
+    Y = np.cumsum(rng.standard_normal((2, L - 9, D)), 1) / np.sqrt(L * D)
+    Xt, Yt = (torch.tensor(v, device="cuda", dtype=torch.float32) for v in (X, Y))
+
+    def levels():
+        return [ops.sig_gram(Xt, Yt, M, order=order, base=base).cpu().numpy(),
+                ops.sig_gram(Xt, None, M, order=order, base=base).cpu().numpy(),
+                ops.sig_diag(Xt, M, order=order, base=base).cpu().numpy()]
+
+    split = levels()
+    monkeypatch.setenv("GPSIG_HO_SPLIT", "0")
+    plain = levels()
+    for g, r in zip(split, plain):
+        for m in range(1, M + 1):
+            assert np.abs(g[m] - r[m]).max() <= 2e-6 * np.abs(r[m]).max(), m
