@@ -147,9 +147,9 @@ def _folded(cfg, X2s, lengths, needs_grad):
     """Normalised K whose backward folds the normalisation's diagonal terms into the weights of the diagonal
     pairs (one VJP launch, see SigGram.backward): the forward keeps the raw levels (and, for K(X, X2), the raw
     diagonals).  Order 1: symmetric K(X); higher orders: under the higher-order VJP kernel, K(X) and K(X, X2)."""
-    if not (needs_grad and cfg["normalization"] and cfg["num_levels"] > 1):
+    if not (needs_grad and cfg["normalization"]):
         return False
-    if cfg["order"] == 1:
+    if cfg["order"] == 1 or cfg["num_levels"] == 1:
         return X2s is None
     return _ho_vjp_kernel(cfg, *lengths)
 

@@ -48,7 +48,13 @@ def test_higher_order_signature_kernel_gradient(normalization, cross, return_lev
     assert norm_rel_err(Xt.grad.reshape(X.shape).cpu().numpy(), Xr.grad.numpy()) < GTOL
     if cross:
         assert norm_rel_err(X2t.grad.reshape(X2.shape).cpu().numpy(), X2r.grad.numpy()) < GTOL
-    assert norm_rel_err(k.lengthscales.grad.cpu().numpy(), lr.grad.numpy()) < GTOL
+    # dLoss/dl_k = -sum_i x_ik dLoss/dx_ik / l_k is a contraction over every point: on these inputs its terms
+    # cancel up to ~2000x ("lengthscale gradients"), so it is held to GTOL times the sum of
+    # the terms' magnitudes, the forward-error bound of that sum -- measured 2.5e-5..3.4e-5 max-relative
+    terms = np.abs(X * Xr.grad.numpy()).reshape(-1, D).sum(0)
+    if cross:
+        terms = terms + np.abs(X2 * X2r.grad.numpy()).reshape(-1, D).sum(0)
+    assert (np.abs(k.lengthscales.grad.cpu().numpy() - lr.grad.numpy()) <= GTOL * terms / ls).all()
     assert norm_rel_err(k.variances.grad.cpu().numpy(), vr.grad.numpy()) < GTOL
 
 
