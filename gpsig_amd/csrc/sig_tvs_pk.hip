@@ -133,6 +133,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(INCR ? GPSIG
   }
 
   const int ncell = a.l - 1;
+  bool far = false;  // wave-uniform: the previous step had some |q| >= TVS_CORNER (no increments)
   for (int s = 0; s < ncell; ++s) {
     // keeps the component reads inside the loop (hoisted, LT x ZS of them would not fit in registers)
     asm volatile("" ::: "memory");
@@ -140,9 +141,10 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(INCR ? GPSIG
 #pragma unroll
     for (int q = 0; q < DP; ++q) dx[q] = q < d ? ld(s, d + q) : splat2(0.f);
     const f2 g = ld(s, 2 * d + 1);
-    const bool anch = (s % ANCHOR) == ANCHOR - 1;
+    const bool anch = (s % ANCHOR) == ANCHOR - 1 || far;
     f2 x1[DP];
     if (anch) ldx(s + 1, x1);
+    uint64_t farm = 0;  // lanes with some |q| >= TVS_CORNER this step (no increments; a scalar mask)
     // components in (level, stage) order; the order-1 recursion (signature_algs.py:115-127) is folded
     // in as each seed is produced
 #pragma unroll
@@ -209,20 +211,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(INCR ? GPSIG
           Ep[k] = Epn;
         } else if (anch) {
           exact(k, x1, kc[k], Ep[k]);  // re-anchor the recurrences every ANCHOR cells
-        } else if ((!INCR && wide && __builtin_amdgcn_ballot_w64(mx >= TVS_CORNER) != 0) ||
-                   __builtin_amdgcn_ballot_w64((kc[k][0] < 1e-30f && qv[0] > 0.f) || (kc[k][1] < 1e-30f && qv[1] > 0.f))) {
-          // exact point values instead of the carry k (1 + expm1(q)): steps with |q| >= TVS_CORNER (the
-          // rounding of q costs |q| eps of the exponent per step), and a carried k below 1e-30 about to grow
-          // (once underflowed it stays 0 while the exact value may reach O(1) before the next anchor: a path
-          // walking towards a far inducing point)
-          f2 xr[DP];
-          ldx(s + 1, xr);
-          exact(k, xr, kc[k], Ep[k]);
         } else if constexpr (INCR) {
           kc[k] = fma2(kc[k], Eq, kc[k]);
           Ep[k] = fma2(Ep[k], Ec, Ep[k] + Ec);
         } else {
           kc[k] = kc[k] + m;
+          farm |= __builtin_amdgcn_ballot_w64(mx >= TVS_CORNER);
         }
         if (st == 0) {
           prev = m;
@@ -234,6 +228,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(INCR ? GPSIG
       }
       K[i] += prev;
     }
+    // (no increments) a step with some |q| >= TVS_CORNER re-anchors the next one: the rounding of q costs
+    // |q| eps of the exponent per carried step, and a carry grown from an underflowed 0 would stay 0 (a path
+    // walking towards a far inducing point).  One carried step of that error is at the fp32 noise level,
+    // and below TVS_CORNER a carry can grow at most e^(2 x 31) between anchors, so one that underflowed
+    // stays below 1e-11: negligible.  The anchor's own path: a second exact evaluation in or after the
+    // component loop cost the kernel its third wave per SIMD (168 -> 188 VGPRs at D = 5, M = 5).
+    if constexpr (!INCR) far = farm != 0;
   }
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -584,16 +585,12 @@ __global__ __launch_bounds__(64) void tvs_wide_kernel(TvsWideArgs a) {
         }
       } else if (anch) {
         exact_all(s + 1, kc, Ep, nullptr, s2c, ppc);  // re-anchor the recurrences every ANCHOR cells
-      } else if ((!INCR && wide && __builtin_amdgcn_ballot_w64(mx >= TVS_CORNER) != 0) || [&] {
-                   bool t = false;
-#pragma unroll
-                   for (int k = 0; k < LT; ++k) t = t || (kc[k] < 1e-30f && qv[k] > 0.f);
-                   return __builtin_amdgcn_ballot_w64(t) != 0;
-                 }()) {
-        // exact point values instead of the carry k (1 + expm1(q)): (a) steps with |q| >= TVS_CORNER, where
-        // the rounding of q (relative) is |q| eps in the exponent per step; (b) a carried k below 1e-30 about
-        // to grow (a path walking towards a far inducing point): once underflowed, the carry stays 0 while the
-        // exact value may reach O(1) before the next anchor
+      } else if (!INCR && wide && __builtin_amdgcn_ballot_w64(mx >= TVS_CORNER) != 0) {
+        // exact point values instead of the carry k (1 + expm1(q)) on steps with |q| >= TVS_CORNER: the
+        // rounding of q costs |q| eps of the exponent per carried step, and a carry grown from an underflowed
+        // 0 would stay 0 (a path walking towards a far inducing point).  Below TVS_CORNER a carry can grow at
+        // most e^(2 x 31) between anchors, so one that underflowed stays below 1e-11: negligible.  (INCR: the
+        // corner regime above takes every step with |q| >= TVS_CORNER.)
         exact_all(s + 1, kc, Ep, nullptr, s2c, ppc);
       } else {
 #pragma unroll
