@@ -89,6 +89,9 @@ SIGNATURES = {
     "gpsig_signature_channels": (ctypes.c_longlong, [_I, _I]),
     "gpsig_signature": (_I, [_P, _I, _I, _I, _I, _P, _P]),
     "gpsig_signature_vjp": (_I, [_P, _I, _I, _I, _I, _P, _P, _P]),
+    "gpsig_signature_workspace_bytes": (_SZ, [_I, _I, _I, _I]),
+    "gpsig_signature_ex": (_I, [_P, _I, _I, _I, _I, _P, _P, _SZ, _P]),
+    "gpsig_signature_vjp_ex": (_I, [_P, _I, _I, _I, _I, _P, _P, _P, _SZ, _P]),
     "gpsig_gemm_f32": (_I, [_I, _I, _I, _I, _I, _F, _P, ctypes.c_longlong, _P, ctypes.c_longlong, _F, _P,
                             ctypes.c_longlong, _P]),
     "gpsig_gemm_splitk_bytes": (_SZ, [_I, _I, _I]),

@@ -132,16 +132,19 @@ GPSIG_DEV double ld_l2_d(const double *p) { return __hip_atomic_load(p, __ATOMIC
 // lane 0 handing its left column of R to the next block the same way (lane 63's right boundary).  The
 // cells, recurrences and summation order within a cell are those of one block, so the result does not
 // depend on the blocking beyond the order of the per-row atomics.
-template <int DP, int W, int REP, bool COLS, int MODE = 0>
-__global__ __launch_bounds__(256) void pde_adj_kernel(PdeBwdArgs p) {
+// V: the K scheme, a compile-time variant of the body (a runtime select per cell cost two v_cndmask per
+// fp64 value): 0 the first-order scheme, 1 the second-order scheme (solver 1), 2 first order with the
+// second-order formula on the diagonal cells (k(x, x) with solver 0, as the forward's hybrid).
+template <int DP, int W, int REP, bool COLS, int MODE, int V>
+__device__ __forceinline__ void pde_adj_body(const PdeBwdArgs &p, double *ldsd) {
   static_assert(W % REP == 0, "a lane owns whole coarse columns");
   constexpr bool TILE = DP == 0;
   constexpr int DPA = TILE ? 1 : DP;
   constexpr int WC = W / REP;
+  constexpr int WC2 = (WC + 1) / 2;  // coarse columns in packed fp32 pairs (the contractions)
   constexpr int H = pde_chunk<W, REP>();
   constexpr int FW = W + REP;  // front words per lane: up[W], last[0 .. REP-2], corner_prev
   constexpr int CB = 64 * W;   // fine columns per block
-  extern __shared__ __attribute__((aligned(16))) double ldsd[];
   const int lane = threadIdx.x & 63;
   const int wave = wave_uniform(threadIdx.x >> 6);
   const bool diag = p.pair_mode == GPSIG_PAIRS_DIAG;
@@ -188,46 +191,50 @@ __global__ __launch_bounds__(256) void pde_adj_kernel(PdeBwdArgs p) {
 
   // the current column block: first fine column, lanes used, y increments of the lane's coarse columns
   int c0 = 0, U = 0;
-  float dy[WC][DPA];
-  double dyd[WC][DPA];  // fp64 copies for the contractions (converted once, not per cell)
+  f2 dyp[WC2][DPA];  // y increments of the lane's coarse columns as packed pairs (2 w2, 2 w2 + 1)
   auto load_block = [&](int blk) {
     c0 = blk * CB;
     U = (J - c0 + W - 1) / W;
     U = U < 64 ? U : 64;
     if constexpr (!TILE) {
+      // columns past the sequence (the lane straddling J, lanes past it) take increment 0: their R stays
+      // the boundary value 1 exactly (1 + 1 - 1), no per-cell guard, and they contract with dy = 0
 #pragma unroll
-      for (int w = 0; w < WC; ++w) {
-        int cj = c0 / REP + lane * WC + w;
-        cj = cj < JC - 1 ? cj : JC - 1;
+      for (int w = 0; w < 2 * WC2; ++w) {
+        const int cj = c0 / REP + lane * WC + w;
+        const bool in = w < WC && cj < JC;
+        const int cjc = cj < JC ? cj : JC - 1;
 #pragma unroll
-        for (int k = 0; k < DP; ++k) {
-          dy[w][k] = k < d ? y[(cj + 1) * d + k] - y[cj * d + k] : 0.0f;
-          dyd[w][k] = (double)dy[w][k];
-        }
+        for (int k = 0; k < DP; ++k) dyp[w / 2][k][w % 2] = (k < d && in) ? y[(cjc + 1) * d + k] - y[cjc * d + k] : 0.0f;
       }
     }
   };
 
-  const bool s1 = p.solver == 1;
-  const bool hybrid = diag && p.solver == 0;
-  auto incs = [&](int ci, double (&inc)[WC], float (&dxv)[DPA]) {
+  constexpr bool s1 = V == 1, hybrid = V == 2;
+  // x's increments of the rows a chunk of H steps visits in this lane (LDS reads batched per chunk, not
+  // one dependent read per step; rows out of range are clamped and never used)
+  auto ldx_chunk = [&](int s0c, float (&dxc)[H][DPA]) {
+#pragma unroll
+    for (int h = 0; h < H; ++h) {
+      int ci = s0c + h - lane;
+      ci = ci < 0 ? 0 : (ci < IC ? ci : IC - 1);
+#pragma unroll
+      for (int k = 0; k < DPA; ++k) dxc[h][k] = TILE ? 0.0f : dxs[ci * DP + k];
+    }
+  };
+  auto incs = [&](int ci, double (&inc)[WC], const float (&dxv)[DPA]) {
     if constexpr (TILE) {
 #pragma unroll
       for (int w = 0; w < WC; ++w) {
-        int cj = c0 / REP + lane * WC + w;
-        cj = cj < JC - 1 ? cj : JC - 1;
-        inc[w] = (double)tile_inc_b(itile, p.inc_ld, sub, ci, cj) * inv_factor;
+        const int cj = c0 / REP + lane * WC + w;
+        inc[w] = cj < JC ? (double)tile_inc_b(itile, p.inc_ld, sub, ci, cj) * inv_factor : 0.0;
       }
-      dxv[0] = 0.0f;
     } else {
-      const float *dxr = dxs + ci * DP;
-#pragma unroll
-      for (int k = 0; k < DP; ++k) dxv[k] = dxr[k];
 #pragma unroll
       for (int w = 0; w < WC; ++w) {
         float incf = 0.0f;
 #pragma unroll
-        for (int k = 0; k < DP; ++k) incf = __builtin_fmaf(dxv[k], dy[w][k], incf);
+        for (int k = 0; k < DP; ++k) incf = __builtin_fmaf(dxv[k], dyp[w / 2][k][w % 2], incf);
         inc[w] = (double)incf * inv_factor;
       }
     }
@@ -243,7 +250,8 @@ __global__ __launch_bounds__(256) void pde_adj_kernel(PdeBwdArgs p) {
     for (int r = 0; r < REP; ++r) last[r] = 1.0;
     corner_prev = 1.0;
   };
-  auto kstep = [&](int s, float (&kc)[REP][W]) {
+  // inco: the step's coarse increments (pass B's R sweep of the same step reuses them)
+  auto kstep = [&](int s, const float (&dxv)[DPA], float (&kc)[REP][W], double (&inco)[WC]) {
     double left[REP];
 #pragma unroll
     for (int r = 0; r < REP; ++r) left[r] = lane_prev(last[r]);
@@ -257,13 +265,13 @@ __global__ __launch_bounds__(256) void pde_adj_kernel(PdeBwdArgs p) {
     const int ci = s - lane;
     if (ci >= 0 && ci < IC && lane < U) {
       double inc[WC], A[WC], B[WC];
-      float dxv[DPA];
       incs(ci, inc, dxv);
 #pragma unroll
       for (int w = 0; w < WC; ++w) {
+        inco[w] = inc[w];
         const double inc2 = inc[w] * inc[w];
         A[w] = s1 ? 1.0 + 0.5 * inc[w] + (1.0 / 12) * inc2 : inc[w];
-        B[w] = s1 ? 1.0 - (1.0 / 12) * inc2 : inc[w] - 1.0;
+        B[w] = s1 ? 1.0 - (1.0 / 12) * inc2 : inc[w] - 1.0;  // (compile-time selects)
       }
 #pragma unroll
       for (int r = 0; r < REP; ++r) {
@@ -275,7 +283,7 @@ __global__ __launch_bounds__(256) void pde_adj_kernel(PdeBwdArgs p) {
         for (int w = 0; w < W; ++w) {
           const double upw = up[w];
           double kn;
-          if (s1) {
+          if constexpr (s1) {
             kn = (upw + lft) * A[w / REP] - cor * B[w / REP];
           } else {
             kn = (upw + lft) + cor * B[w / REP];
@@ -310,17 +318,19 @@ __global__ __launch_bounds__(256) void pde_adj_kernel(PdeBwdArgs p) {
 #pragma unroll
       for (int r = 0; r + 1 < REP; ++r) f[(W + r) * 64 + lane] = (float)last[r];
       f[(W + REP - 1) * 64 + lane] = (float)corner_prev;
+      float dxc[H][DPA];
+      ldx_chunk(s0, dxc);
 #pragma unroll
       for (int h = 0; h < H; ++h) {
+        // steps past nsteps (the last chunk's tail) touch no cell: ci >= IC in every lane used
         float kc[REP][W];
+        double incd[WC];
         const int s = s0 + h;
-        if (s < nsteps) {
-          kstep(s, kc);
-          const int ci = s - 63;  // lane 63 (a full block) hands its right column on
-          if (kout && lane == 63 && ci >= 0 && ci < IC) {
+        kstep(s, dxc[h], kc, incd);
+        const int ci = s - 63;  // lane 63 (a full block) hands its right column on
+        if (kout && lane == 63 && ci >= 0 && ci < IC) {
 #pragma unroll
-            for (int r = 0; r < REP; ++r) kout[ci * REP + r + 1] = last[r];
-          }
+          for (int r = 0; r < REP; ++r) kout[ci * REP + r + 1] = last[r];
         }
       }
     }
@@ -345,7 +355,8 @@ __global__ __launch_bounds__(256) void pde_adj_kernel(PdeBwdArgs p) {
   const double gts = TILE ? (diag ? 2.0 : 1.0) * inv_factor * (double)g / (double)(1 << (2 * sub)) : 0.0;
   // ---- pass B: blocks right to left, chunks backwards; the R sweep runs in its own step order
   double ru[W], rlast[REP], rcorner;
-  double gcol[WC][DPA];
+  double gcol[WC][DPA];  // column sums S dx: fp32 pairs within a chunk (gcp), fp64 across chunks
+  f2 gcp[WC2][DPA];
   for (int blk = nblk - 1; ok && blk >= 0; --blk) {
     load_block(blk);
     kin = blk > 0 ? kbr + (long long)blk * (I + 1) : nullptr;
@@ -362,21 +373,36 @@ __global__ __launch_bounds__(256) void pde_adj_kernel(PdeBwdArgs p) {
 #pragma unroll
       for (int k = 0; k < DP; ++k) gcol[w][k] = 0.0;
     const int nsteps = IC + U - 1;
+    // the chunk's front, loaded one chunk ahead (the restore would otherwise wait on HBM at every chunk)
+    float fv[FW];
+    auto ldfront = [&](int c0s) {
+      const float *f = fb + (long long)(c0s / H) * FW * 64;
+#pragma unroll
+      for (int e = 0; e < FW; ++e) fv[e] = f[e * 64 + lane];
+    };
+    ldfront(((nsteps - 1) / H) * H);
     for (int s0 = ((nsteps - 1) / H) * H; s0 >= 0; s0 -= H) {
-      const float *f = fb + (long long)(s0 / H) * FW * 64;
 #pragma unroll
-      for (int w = 0; w < W; ++w) up[w] = (double)f[w * 64 + lane];
+      for (int w = 0; w < W; ++w) up[w] = (double)fv[w];
 #pragma unroll
-      for (int r = 0; r + 1 < REP; ++r) last[r] = (double)f[(W + r) * 64 + lane];
+      for (int r = 0; r + 1 < REP; ++r) last[r] = (double)fv[W + r];
       last[REP - 1] = up[W - 1];
-      corner_prev = (double)f[(W + REP - 1) * 64 + lane];
+      corner_prev = (double)fv[W + REP - 1];
+      if (s0 >= H) ldfront(s0 - H);
       float kc[H][REP][W];
+      double incH[H][WC];
 #pragma unroll
-      for (int h = 0; h < H; ++h)
-        if (s0 + h < nsteps) kstep(s0 + h, kc[h]);
+      for (int w2 = 0; w2 < WC2; ++w2)
+#pragma unroll
+        for (int k = 0; k < DPA; ++k) gcp[w2][k] = splat2(0.0f);
+      // steps past nsteps touch no cell (ci >= IC in every lane used), and in the R sweep they come first,
+      // on the boundary values 1: no guards
+      float dxc[H][DPA];
+      ldx_chunk(s0, dxc);
+#pragma unroll
+      for (int h = 0; h < H; ++h) kstep(s0 + h, dxc[h], kc[h], incH[h]);
 #pragma unroll
       for (int h = H - 1; h >= 0; --h) {
-        if (s0 + h >= nsteps) continue;
         double right[REP];
 #pragma unroll
         for (int r = 0; r < REP; ++r) right[r] = lane_next_d(rlast[r]);
@@ -390,11 +416,9 @@ __global__ __launch_bounds__(256) void pde_adj_kernel(PdeBwdArgs p) {
         const int ci = s0 + h - lane;
         if (ci >= 0 && ci < IC && lane < U) {
           double inc[WC], S[WC];
-          float dxv[DPA];
-          incs(ci, inc, dxv);
 #pragma unroll
           for (int w = 0; w < WC; ++w) {
-            inc[w] -= 1.0;
+            inc[w] = incH[h][w] - 1.0;  // the K step's increments (same row ci)
             S[w] = 0.0;
           }
 #pragma unroll
@@ -403,16 +427,14 @@ __global__ __launch_bounds__(256) void pde_adj_kernel(PdeBwdArgs p) {
             double cor = r == REP - 1 ? rcorner : right[r + 1];
 #pragma unroll
             for (int w = W - 1; w >= 0; --w) {
-              const int c = c0 + lane * W + w;
               const double upw = ru[w];
               const double rn = (upw + rgt) + cor * inc[w / REP];
-              if (c < J) {  // columns >= J keep the boundary value 1
-                // KK[i][c] = K(i, c) * R(i+1, c+1) = K[i][c] * K_rev[I-1-i][J-1-c]
-                S[w / REP] = __builtin_fma((double)kc[h][r][w], cor, S[w / REP]);
-                cor = upw;
-                rgt = rn;
-                ru[w] = rn;
-              }
+              // KK[i][c] = K(i, c) * R(i+1, c+1) = K[i][c] * K_rev[I-1-i][J-1-c] (columns >= J: R = 1,
+              // their sums meet dy = 0 and are not stored)
+              S[w / REP] = __builtin_fma((double)kc[h][r][w], cor, S[w / REP]);
+              cor = upw;
+              rgt = rn;
+              ru[w] = rn;
             }
             rlast[r] = rgt;
           }
@@ -434,25 +456,38 @@ __global__ __launch_bounds__(256) void pde_adj_kernel(PdeBwdArgs p) {
               }
             }
           } else {
-          double grow[DP], dxd[DP];
+            // contractions on packed fp32 pairs of coarse columns: the row sums (over the lane's WC columns,
+            // then fp64 in the LDS row accumulators) and the column sums (fp32 over a chunk's H rows, then fp64)
+            f2 Sp[WC2], gr[DP];
 #pragma unroll
-          for (int k = 0; k < DP; ++k) {
-            grow[k] = 0.0;
-            dxd[k] = (double)dxv[k];
-          }
-#pragma unroll
-          for (int w = 0; w < WC; ++w)
+            for (int w2 = 0; w2 < WC2; ++w2)
+              Sp[w2] = (f2){(float)S[2 * w2], 2 * w2 + 1 < WC ? (float)S[(2 * w2 + 1) % WC] : 0.0f};
 #pragma unroll
             for (int k = 0; k < DP; ++k) {
-              grow[k] = __builtin_fma(S[w], dyd[w][k], grow[k]);
-              if constexpr (COLS) gcol[w][k] = __builtin_fma(S[w], dxd[k], gcol[w][k]);
+              gr[k] = Sp[0] * dyp[0][k];
+#pragma unroll
+              for (int w2 = 1; w2 < WC2; ++w2) gr[k] = fma2(Sp[w2], dyp[w2][k], gr[k]);
             }
 #pragma unroll
-          for (int k = 0; k < DP; ++k)
-            if (k < d) atomicAdd(gacc + ci * DP + k, grow[k]);
+            for (int k = 0; k < DP; ++k)
+              if (k < d) atomicAdd(gacc + ci * DP + k, (double)(gr[k][0] + gr[k][1]));
+            if constexpr (COLS) {
+#pragma unroll
+              for (int k = 0; k < DP; ++k) {
+                const f2 dxk = splat2(dxc[h][k]);
+#pragma unroll
+                for (int w2 = 0; w2 < WC2; ++w2) gcp[w2][k] = fma2(Sp[w2], dxk, gcp[w2][k]);
+              }
+            }
           }
         }
         rcorner = right[0];
+      }
+      if constexpr (COLS && !TILE) {
+#pragma unroll
+        for (int w = 0; w < WC; ++w)
+#pragma unroll
+          for (int k = 0; k < DP; ++k) gcol[w][k] += (double)gcp[w / 2][k][w % 2];
       }
     }
     if constexpr (COLS && !TILE) {
@@ -488,6 +523,14 @@ __global__ __launch_bounds__(256) void pde_adj_kernel(PdeBwdArgs p) {
       const double gc = r < IC ? gacc[r * DP + k] : 0.0;
       unsafeAtomicAdd(gxa + (long long)r * d + k, (float)(sx * (gp - gc)));
     }
+}
+
+template <int DP, int W, int REP, bool COLS, int MODE = 0>
+__global__ __launch_bounds__(256) void pde_adj_kernel(PdeBwdArgs p) {
+  extern __shared__ __attribute__((aligned(16))) double ldsd[];
+  if (p.solver == 1) pde_adj_body<DP, W, REP, COLS, MODE, 1>(p, ldsd);
+  else if (p.pair_mode == GPSIG_PAIRS_DIAG) pde_adj_body<DP, W, REP, COLS, MODE, 2>(p, ldsd);
+  else pde_adj_body<DP, W, REP, COLS, MODE, 0>(p, ldsd);
 }
 
 template <int DP, int W, int REP, int MODE>

@@ -6,7 +6,9 @@
 //   S(x) = exp(dx_1) (x) exp(dx_2) (x) ... (x) exp(dx_{L-1}),   exp(h)_m = h^{(x)m} / m!,
 // each level flattened first-index-major (iisignature's layout), concatenated.
 //
-// One workgroup per path; the level tensors live in LDS.  Per increment h the levels are updated in
+// One workgroup per path; the level tensors live in LDS, or (GLB, past the 160 KiB of a CU's LDS) in a
+// per-path slab of global memory (L2-resident at the sizes it takes over; the workgroup barriers order
+// its accesses as they do the LDS ones).  Per increment h the levels are updated in
 // place from the top level down (Chen's identity):
 //   S_m[i_1..i_m] += sum_{j<m} S_j[i_1..i_j] h[i_{j+1}] ... h[i_m] / (m-j)!
 // every entry independently (one thread per entry, the prefix sums read the not-yet-updated lower
@@ -20,6 +22,9 @@ struct SigFeatArgs {
   int n, l, d, depth;
   float *out;      // (n, total)
   int total;       // sum_{m=1}^{depth} d^m
+  float *glb;      // GLB: per-path slabs of `stride` floats for the paths [path0, path0 + gridDim.x)
+  long long stride;
+  int path0;
 };
 
 // Digits of a multi-index in base d (indices < 2^32 / d; tensors here are < 2^14 entries): quotient by a multiply-high with
@@ -31,9 +36,11 @@ struct DivD {
   __device__ int div(int v) const { return d == 1 ? v : (int)__umulhi((unsigned)v, m); }
 };
 
+template <bool GLB>
 __global__ __launch_bounds__(256) void sig_features_kernel(SigFeatArgs a) {
-  extern __shared__ __attribute__((aligned(16))) float S[];  // [h (d) | level 1 | level 2 | ...]
-  const int path = blockIdx.x, tid = threadIdx.x, nth = blockDim.x;
+  extern __shared__ __attribute__((aligned(16))) float lds_s[];  // [h (d) | level 1 | level 2 | ...]
+  const int path = a.path0 + (int)blockIdx.x, tid = threadIdx.x, nth = blockDim.x;
+  float *S = GLB ? a.glb + (long long)blockIdx.x * a.stride : lds_s;
   const int d = a.d, M = a.depth;
   float *h = S;
   float *lev = S + d;
@@ -96,10 +103,12 @@ __device__ inline float group_reduce(float v, int G) {
   return v;
 }
 
+template <bool GLB>
 __global__ __launch_bounds__(256) void sig_features_bwd_kernel(SigFeatArgs a, const float *__restrict__ gout,
                                                                float *__restrict__ gX) {
-  extern __shared__ __attribute__((aligned(16))) float sh[];
-  const int path = blockIdx.x, tid = threadIdx.x, nth = blockDim.x;
+  extern __shared__ __attribute__((aligned(16))) float lds_s[];
+  const int path = a.path0 + (int)blockIdx.x, tid = threadIdx.x, nth = blockDim.x;
+  float *sh = GLB ? a.glb + (long long)blockIdx.x * a.stride : lds_s;
   const int d = a.d, M = a.depth, tot = a.total;
   float *h = sh, *gh = sh + d;
   float *lev = sh + 2 * d, *adj = lev + tot, *gE = adj + tot;
@@ -261,27 +270,10 @@ __global__ __launch_bounds__(256) void sig_features_bwd_kernel(SigFeatArgs a, co
 
 using namespace gpsig;
 
-extern "C" int gpsig_signature_vjp(const float *X, int n, int l, int d, int depth, const float *gout, float *gX,
-                                   gpsig_stream_t stream) {
-  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
-  if (!X || !gout || !gX || n <= 0 || l < 1 || d <= 0 || depth < 1) return GPSIG_EINVAL;
-  if (depth > 16) return GPSIG_EUNSUPPORTED;
-  long long total = 0, p = 1;
-  for (int m = 1; m <= depth; ++m) {
-    p *= d;
-    total += p;
-  }
-  const size_t lds = (size_t)(4 * total + 2 * d) * sizeof(float);
-  if (lds > 64 * 1024) return GPSIG_EUNSUPPORTED;
-  SigFeatArgs a{X, n, l, d, depth, nullptr, (int)total};
-  // one wave per path while the top level fits a few entries per lane (barriers stay wave-local)
-  const int nth = (total - (total - 1) / d) <= 256 ? 64 : 256;
-  hipLaunchKernelGGL(sig_features_bwd_kernel, dim3((unsigned)n), dim3(nth), lds, s, a, gout, gX);
-  return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
-}
-
-extern "C" long long gpsig_signature_channels(int d, int depth) {
-  if (d <= 0 || depth <= 0) return 0;
+namespace {
+constexpr size_t SIG_LDS_MAX = 160 * 1024;               // a CU's LDS
+constexpr size_t SIG_GLB_BUDGET = (size_t)1 << 30;       // per launch chunk of paths (GLB slabs)
+long long sig_total(int d, int depth) {
   long long t = 0, p = 1;
   for (int m = 1; m <= depth; ++m) {
     p *= d;
@@ -289,16 +281,94 @@ extern "C" long long gpsig_signature_channels(int d, int depth) {
   }
   return t;
 }
+// floats of one path's level storage: forward [h | levels], backward [h | gh | levels | adjoints | dE | E]
+long long sig_slab_floats(long long total, int d, bool vjp) {
+  const long long f = vjp ? 4 * total + 2 * d : total + d;
+  return (f + 63) & ~63LL;  // 256-byte aligned slabs
+}
+bool sig_in_lds(long long total, int d, bool vjp) { return (size_t)(vjp ? 4 * total + 2 * d : total + d) * 4 <= SIG_LDS_MAX; }
+int sig_chunk_paths(long long slab, int n) {
+  long long c = (long long)(SIG_GLB_BUDGET / ((size_t)slab * sizeof(float)));
+  if (c < 1) c = 1;
+  return (int)(c < n ? c : n);
+}
+bool sig_args_ok(long long total, int d, int depth) {
+  // entries are indexed in int, digits by a multiply-high valid below 2^32 / d
+  return depth <= 16 && total > 0 && total < (1LL << 31) / 4 && (long long)d * total < (1LL << 32);
+}
+}  // namespace
 
-extern "C" int gpsig_signature(const float *X, int n, int l, int d, int depth, float *out, gpsig_stream_t stream) {
+extern "C" long long gpsig_signature_channels(int d, int depth) {
+  if (d <= 0 || depth <= 0) return 0;
+  return sig_total(d, depth);
+}
+
+extern "C" size_t gpsig_signature_workspace_bytes(int n, int d, int depth, int vjp) {
+  if (n <= 0 || d <= 0 || depth <= 0 || depth > 16) return 0;
+  const long long total = sig_total(d, depth);
+  if (sig_in_lds(total, d, vjp != 0)) return 0;
+  const long long slab = sig_slab_floats(total, d, vjp != 0);
+  return (size_t)sig_chunk_paths(slab, n) * (size_t)slab * sizeof(float);
+}
+
+extern "C" int gpsig_signature_ex(const float *X, int n, int l, int d, int depth, float *out, void *workspace,
+                                  size_t workspace_bytes, gpsig_stream_t stream) {
   hipStream_t s = reinterpret_cast<hipStream_t>(stream);
   if (!X || !out || n <= 0 || l < 1 || d <= 0 || depth < 1) return GPSIG_EINVAL;
   if (depth > 16) return GPSIG_EUNSUPPORTED;
-  const long long total = gpsig_signature_channels(d, depth);
-  const size_t lds = (size_t)(total + d) * sizeof(float);
-  if (lds > 64 * 1024) return GPSIG_EUNSUPPORTED;
-  SigFeatArgs a{X, n, l, d, depth, out, (int)total};
+  const long long total = sig_total(d, depth);
+  if (!sig_args_ok(total, d, depth)) return GPSIG_EUNSUPPORTED;
+  SigFeatArgs a{X, n, l, d, depth, out, (int)total, nullptr, 0, 0};
   const int nth = (total - (total - 1) / d) <= 256 ? 64 : 256;  // top level d^depth entries
-  hipLaunchKernelGGL(sig_features_kernel, dim3((unsigned)n), dim3(nth), lds, s, a);
+  if (sig_in_lds(total, d, false)) {
+    const size_t lds = (size_t)(total + d) * sizeof(float);
+    hipLaunchKernelGGL(sig_features_kernel<false>, dim3((unsigned)n), dim3(nth), lds, s, a);
+    return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
+  }
+  a.stride = sig_slab_floats(total, d, false);
+  const int chunk = sig_chunk_paths(a.stride, n);
+  if (!workspace || workspace_bytes < (size_t)chunk * (size_t)a.stride * sizeof(float)) return GPSIG_EWORKSPACE;
+  a.glb = static_cast<float *>(workspace);
+  for (int p0 = 0; p0 < n; p0 += chunk) {
+    a.path0 = p0;
+    const int np = n - p0 < chunk ? n - p0 : chunk;
+    hipLaunchKernelGGL(sig_features_kernel<true>, dim3((unsigned)np), dim3(256), 0, s, a);
+  }
   return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
+}
+
+extern "C" int gpsig_signature(const float *X, int n, int l, int d, int depth, float *out, gpsig_stream_t stream) {
+  return gpsig_signature_ex(X, n, l, d, depth, out, nullptr, 0, stream);
+}
+
+extern "C" int gpsig_signature_vjp_ex(const float *X, int n, int l, int d, int depth, const float *gout, float *gX,
+                                      void *workspace, size_t workspace_bytes, gpsig_stream_t stream) {
+  hipStream_t s = reinterpret_cast<hipStream_t>(stream);
+  if (!X || !gout || !gX || n <= 0 || l < 1 || d <= 0 || depth < 1) return GPSIG_EINVAL;
+  if (depth > 16) return GPSIG_EUNSUPPORTED;
+  const long long total = sig_total(d, depth);
+  if (!sig_args_ok(total, d, depth)) return GPSIG_EUNSUPPORTED;
+  SigFeatArgs a{X, n, l, d, depth, nullptr, (int)total, nullptr, 0, 0};
+  // one wave per path while the top level fits a few entries per lane (barriers stay wave-local)
+  const int nth = (total - (total - 1) / d) <= 256 ? 64 : 256;
+  if (sig_in_lds(total, d, true)) {
+    const size_t lds = (size_t)(4 * total + 2 * d) * sizeof(float);
+    hipLaunchKernelGGL(sig_features_bwd_kernel<false>, dim3((unsigned)n), dim3(nth), lds, s, a, gout, gX);
+    return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
+  }
+  a.stride = sig_slab_floats(total, d, true);
+  const int chunk = sig_chunk_paths(a.stride, n);
+  if (!workspace || workspace_bytes < (size_t)chunk * (size_t)a.stride * sizeof(float)) return GPSIG_EWORKSPACE;
+  a.glb = static_cast<float *>(workspace);
+  for (int p0 = 0; p0 < n; p0 += chunk) {
+    a.path0 = p0;
+    const int np = n - p0 < chunk ? n - p0 : chunk;
+    hipLaunchKernelGGL(sig_features_bwd_kernel<true>, dim3((unsigned)np), dim3(256), 0, s, a, gout, gX);
+  }
+  return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
+}
+
+extern "C" int gpsig_signature_vjp(const float *X, int n, int l, int d, int depth, const float *gout, float *gX,
+                                   gpsig_stream_t stream) {
+  return gpsig_signature_vjp_ex(X, n, l, d, depth, gout, gX, nullptr, 0, stream);
 }

@@ -495,7 +495,9 @@ def signature(X: torch.Tensor, depth: int) -> torch.Tensor:
     out = torch.empty((n, int(lib.gpsig_signature_channels(d, depth))), dtype=torch.float32, device=X.device)
     if n == 0:
         return out
-    L.check(lib.gpsig_signature(X.data_ptr(), n, l, d, depth, out.data_ptr(), _stream(X.device)), "gpsig_signature")
+    ws = workspace(X.device, lib.gpsig_signature_workspace_bytes(n, d, depth, 0))  # past the LDS: level slabs
+    L.check(lib.gpsig_signature_ex(X.data_ptr(), n, l, d, depth, out.data_ptr(), ws.data_ptr(), ws.numel(),
+                                   _stream(X.device)), "gpsig_signature")
     return out
 
 
@@ -509,8 +511,9 @@ def signature_vjp(X: torch.Tensor, depth: int, gout: torch.Tensor, gX: torch.Ten
         raise ValueError("gout must be (n, channels)")
     if gX is None:
         gX = torch.zeros((n, l, d), dtype=torch.float32, device=X.device)
-    L.check(lib.gpsig_signature_vjp(X.data_ptr(), n, l, d, depth, gout.data_ptr(), gX.data_ptr(), _stream(X.device)),
-            "gpsig_signature_vjp")
+    ws = workspace(X.device, lib.gpsig_signature_workspace_bytes(n, d, depth, 1))
+    L.check(lib.gpsig_signature_vjp_ex(X.data_ptr(), n, l, d, depth, gout.data_ptr(), gX.data_ptr(), ws.data_ptr(),
+                                       ws.numel(), _stream(X.device)), "gpsig_signature_vjp")
     return gX
 
 

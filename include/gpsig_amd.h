@@ -315,14 +315,28 @@ int gpsig_pde_vjp_fronts_ex(const float *X, int n1, int l1, const float *Y, int 
  * Truncated signatures (replaces iisignature.sig behind iisignature_tensorflow.Sig,
  * gpsig/iisignature_tensorflow.py:87, used by the VOSF Kuf, gpsig/inducing_variables_vosf.py:120-146).
  * X (n, l, d) -> out (n, gpsig_signature_channels(d, depth)): levels 1..depth, each flattened
- * first-index-major, concatenated (iisignature.sig's layout).  Needs (channels + d) * 4 <= 64 KiB.
+ * first-index-major, concatenated (iisignature.sig's layout).  Any size the int32 entry index takes (channels
+ * < 2^29, d channels < 2^32): while (channels + d) * 4 <= 160 KiB the levels live in a CU's LDS, past it in
+ * per-path slabs of the caller's workspace (gpsig_signature_workspace_bytes, 0 for the LDS case).
  */
 long long gpsig_signature_channels(int d, int depth);
 
+/* Workspace of gpsig_signature_ex (vjp = 0) / gpsig_signature_vjp_ex (vjp = 1): 0 when the levels fit the
+ * LDS, else the slabs of one launch chunk of paths (at most 1 GiB, at least one path). */
+size_t gpsig_signature_workspace_bytes(int n, int d, int depth, int vjp);
+
+int gpsig_signature_ex(const float *X, int n, int l, int d, int depth, float *out, void *workspace,
+                       size_t workspace_bytes, gpsig_stream_t stream);
+
+/* gpsig_signature_ex without a workspace: GPSIG_EWORKSPACE past the LDS. */
 int gpsig_signature(const float *X, int n, int l, int d, int depth, float *out, gpsig_stream_t stream);
 
 /* Gradient of gpsig_signature (iisignature.sigbackprop behind the Sig op's gradient): gout (n, channels)
- * = dLoss/dsig; accumulates (+=) gX (n, l, d).  Needs (3 channels + 2 d) * 4 <= 64 KiB. */
+ * = dLoss/dsig; accumulates (+=) gX (n, l, d).  The levels, their adjoints and two tables of the step's
+ * exponential: (4 channels + 2 d) * 4 bytes in LDS up to 160 KiB, past it in the workspace. */
+int gpsig_signature_vjp_ex(const float *X, int n, int l, int d, int depth, const float *gout, float *gX,
+                           void *workspace, size_t workspace_bytes, gpsig_stream_t stream);
+
 int gpsig_signature_vjp(const float *X, int n, int l, int d, int depth, const float *gout, float *gX,
                         gpsig_stream_t stream);
 

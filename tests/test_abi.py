@@ -89,6 +89,14 @@ def test_vjp_and_feature_entry_points_validate_arguments():
     assert lib.gpsig_signature(None, 4, 10, 3, 3, None, None) == L.GPSIG_EINVAL
     assert lib.gpsig_signature_vjp(None, 4, 10, 3, 3, None, None, None) == L.GPSIG_EINVAL
     assert lib.gpsig_signature_channels(5, 3) == 5 + 25 + 125
+    # past the 160 KiB of LDS the levels take per-path workspace slabs (256-byte aligned, <= 1 GiB per launch)
+    assert lib.gpsig_signature_workspace_bytes(4, 5, 5, 0) == 0 and lib.gpsig_signature_workspace_bytes(4, 5, 5, 1) == 0
+    tot = lib.gpsig_signature_channels(6, 6)  # 55 986 coordinates
+    assert lib.gpsig_signature_workspace_bytes(4, 6, 6, 0) == 4 * ((tot + 6 + 63) // 64 * 64) * 4
+    assert lib.gpsig_signature_workspace_bytes(4, 6, 6, 1) == 4 * ((4 * tot + 12 + 63) // 64 * 64) * 4
+    fake = ctypes.c_void_p(256)  # never dereferenced: the workspace check comes before any launch
+    assert lib.gpsig_signature(fake, 4, 10, 6, 6, fake, None) == L.GPSIG_EWORKSPACE
+    assert lib.gpsig_signature_vjp(fake, 4, 10, 6, 6, fake, fake, None) == L.GPSIG_EWORKSPACE
     # J = 18 fine columns at dyadic 1: W = 2 per lane, U = 9 lanes, 9 + 9 - 1 = 17 coarse steps, a front every
     # 32 / (2 * 2) = 8 steps -> 3 fronts of (W + REP) x 64 floats per pair
     assert lib.gpsig_pde_vjp_workspace_bytes(2, 10, 10, 1) == 2 * 3 * (2 + 2) * 64 * 4

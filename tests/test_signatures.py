@@ -30,8 +30,11 @@ def test_torch_signature_oracle_matches_chen():
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("d,depth,L", [(2, 6, 30), (3, 4, 50), (5, 5, 40), (1, 3, 10), (8, 3, 20)])
+@pytest.mark.parametrize("d,depth,L", [(2, 6, 30), (3, 4, 50), (5, 5, 40), (1, 3, 10), (8, 3, 20),
+                                       (6, 6, 12), (40, 3, 8)])
 def test_signature_matches_chen(d, depth, L):
+    """(6, 6) and (40, 3) have 55 986 / 65 640 coordinates: past the 160 KiB of LDS, the levels live in
+    per-path slabs of the workspace (gpsig_signature_workspace_bytes)."""
     from gpsig_amd import ops
     rng = np.random.default_rng(d + depth)
     X = np.cumsum(rng.standard_normal((9, L, d)), 1) / np.sqrt(L)
@@ -45,8 +48,10 @@ def test_signature_matches_chen(d, depth, L):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("d,depth,L", [(2, 4, 12), (3, 3, 20), (5, 3, 15)])
+@pytest.mark.parametrize("d,depth,L", [(2, 4, 12), (3, 3, 20), (5, 3, 15), (4, 7, 8), (12, 4, 6)])
 def test_signature_backprop_matches_autodiff(d, depth, L):
+    """(4, 7) and (12, 4): 21 844 / 22 620 coordinates, the VJP's levels, adjoints and exponential tables
+    (4 x the coordinates) past the LDS, in the workspace slabs."""
     from gpsig_amd import signatures as sg
     rng = np.random.default_rng(10 + d)
     X = np.cumsum(rng.standard_normal((5, L, d)), 1) / np.sqrt(L)
@@ -59,7 +64,7 @@ def test_signature_backprop_matches_autodiff(d, depth, L):
         xa = torch.tensor(X[a], requires_grad=True)
         (ar.signature(xa, depth) * torch.tensor(G[a])).sum().backward()
         ref[a] = xa.grad.numpy()
-    assert norm_rel_err(Xt.grad.cpu().numpy(), ref) < 5e-5
+    assert norm_rel_err(Xt.grad.cpu().numpy(), ref) < 1e-5
 
 
 @pytest.mark.gpu
