@@ -1,8 +1,9 @@
 """GPU parity of the gradients: gpsig_sig_gram_vjp (through gpsig_amd.autograd) vs torch fp64 autodiff
 of the reference graph (oracle/autodiff_ref.py, pinned by finite differences in test_grad_oracle.py).
 
-Criterion: norm-relative max|g32 - g64| <= GTOL * max|g64| per gradient tensor.  The forward is fp32
-(1e-5 bar); a gradient chains one more fp32 sweep, so the bar is 5e-5.
+Criterion: norm-relative max|g32 - g64| <= GTOL * max|g64| per gradient tensor, GTOL = 1e-5 (the
+north_star's fp32 bar, applied to gradients since round 5); the one named exception is in
+test_gram_vjp_shapes, with its measured error.
 """
 import numpy as np
 import pytest
