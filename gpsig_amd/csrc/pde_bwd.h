@@ -119,7 +119,10 @@ __host__ __device__ inline PdeLayout pde_layout_eff(int l1, int l2, int dyadic) 
 inline long long pde_front_floats(int l1, int l2, int dyadic) { return pde_layout_eff(l1, l2, dyadic).pair_floats; }
 
 // LDS of one wave (pair) of the adjoint kernel, in doubles
-__host__ __device__ inline size_t pde_lds_wave_doubles(int IC, int DP) { return ((size_t)IC * DP * 12 + 7) / 8; }
+// (cross pairs: plus the lanes' column sums, 64 x WC x DP doubles: in LDS, not registers, for occupancy)
+__host__ __device__ inline size_t pde_lds_wave_doubles(int IC, int DP, int WC = 0) {
+  return ((size_t)IC * DP * 12 + 7) / 8 + (size_t)64 * WC * DP;
+}
 
 GPSIG_DEV double ld_l2_d(const double *p) { return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); }
 
@@ -176,8 +179,12 @@ __device__ __forceinline__ void pde_adj_body(const PdeBwdArgs &p, double *ldsd) 
   double *kbr = reinterpret_cast<double *>(fr + lay.kb_off);
 
   // LDS: [wave] { coarse-row accumulators (IC x DP doubles) | dx (IC x DP floats) }
-  double *gacc = ldsd + (size_t)wave * pde_lds_wave_doubles(IC, DP);
-  float *dxs = reinterpret_cast<float *>(gacc + (size_t)IC * DP);
+  // LDS: [wave] { coarse-row accumulators (IC x DP doubles) | (COLS) column sums [WC x DP][64] doubles |
+  //               dx (IC x DP floats) }
+  constexpr int GCW = (COLS && !TILE) ? WC : 0;
+  double *gacc = ldsd + (size_t)wave * pde_lds_wave_doubles(IC, DP, GCW);
+  double *gcl = gacc + (size_t)IC * DP;
+  float *dxs = reinterpret_cast<float *>(gcl + (size_t)64 * GCW * DP);
   if constexpr (!TILE) {
     for (int r = lane; r < IC; r += 64) {
 #pragma unroll
@@ -211,18 +218,7 @@ __device__ __forceinline__ void pde_adj_body(const PdeBwdArgs &p, double *ldsd) 
   };
 
   constexpr bool s1 = V == 1, hybrid = V == 2;
-  // x's increments of the rows a chunk of H steps visits in this lane (LDS reads batched per chunk, not
-  // one dependent read per step; rows out of range are clamped and never used)
-  auto ldx_chunk = [&](int s0c, float (&dxc)[H][DPA]) {
-#pragma unroll
-    for (int h = 0; h < H; ++h) {
-      int ci = s0c + h - lane;
-      ci = ci < 0 ? 0 : (ci < IC ? ci : IC - 1);
-#pragma unroll
-      for (int k = 0; k < DPA; ++k) dxc[h][k] = TILE ? 0.0f : dxs[ci * DP + k];
-    }
-  };
-  auto incs = [&](int ci, double (&inc)[WC], const float (&dxv)[DPA]) {
+  auto incs = [&](int ci, double (&inc)[WC]) {
     if constexpr (TILE) {
 #pragma unroll
       for (int w = 0; w < WC; ++w) {
@@ -230,6 +226,10 @@ __device__ __forceinline__ void pde_adj_body(const PdeBwdArgs &p, double *ldsd) 
         inc[w] = cj < JC ? (double)tile_inc_b(itile, p.inc_ld, sub, ci, cj) * inv_factor : 0.0;
       }
     } else {
+      float dxv[DP];
+      const float *dxr = dxs + ci * DP;
+#pragma unroll
+      for (int k = 0; k < DP; ++k) dxv[k] = dxr[k];
 #pragma unroll
       for (int w = 0; w < WC; ++w) {
         float incf = 0.0f;
@@ -251,7 +251,7 @@ __device__ __forceinline__ void pde_adj_body(const PdeBwdArgs &p, double *ldsd) 
     corner_prev = 1.0;
   };
   // inco: the step's coarse increments (pass B's R sweep of the same step reuses them)
-  auto kstep = [&](int s, const float (&dxv)[DPA], float (&kc)[REP][W], double (&inco)[WC]) {
+  auto kstep = [&](int s, float (&kc)[REP][W], double (&inco)[WC]) {
     double left[REP];
 #pragma unroll
     for (int r = 0; r < REP; ++r) left[r] = lane_prev(last[r]);
@@ -265,7 +265,7 @@ __device__ __forceinline__ void pde_adj_body(const PdeBwdArgs &p, double *ldsd) 
     const int ci = s - lane;
     if (ci >= 0 && ci < IC && lane < U) {
       double inc[WC], A[WC], B[WC];
-      incs(ci, inc, dxv);
+      incs(ci, inc);
 #pragma unroll
       for (int w = 0; w < WC; ++w) {
         inco[w] = inc[w];
@@ -318,15 +318,13 @@ __device__ __forceinline__ void pde_adj_body(const PdeBwdArgs &p, double *ldsd) 
 #pragma unroll
       for (int r = 0; r + 1 < REP; ++r) f[(W + r) * 64 + lane] = (float)last[r];
       f[(W + REP - 1) * 64 + lane] = (float)corner_prev;
-      float dxc[H][DPA];
-      ldx_chunk(s0, dxc);
 #pragma unroll
       for (int h = 0; h < H; ++h) {
         // steps past nsteps (the last chunk's tail) touch no cell: ci >= IC in every lane used
         float kc[REP][W];
         double incd[WC];
         const int s = s0 + h;
-        kstep(s, dxc[h], kc, incd);
+        kstep(s, kc, incd);
         const int ci = s - 63;  // lane 63 (a full block) hands its right column on
         if (kout && lane == 63 && ci >= 0 && ci < IC) {
 #pragma unroll
@@ -355,8 +353,7 @@ __device__ __forceinline__ void pde_adj_body(const PdeBwdArgs &p, double *ldsd) 
   const double gts = TILE ? (diag ? 2.0 : 1.0) * inv_factor * (double)g / (double)(1 << (2 * sub)) : 0.0;
   // ---- pass B: blocks right to left, chunks backwards; the R sweep runs in its own step order
   double ru[W], rlast[REP], rcorner;
-  double gcol[WC][DPA];  // column sums S dx: fp32 pairs within a chunk (gcp), fp64 across chunks
-  f2 gcp[WC2][DPA];
+  f2 gcp[WC2][DPA];  // column sums S dx: fp32 pairs within a chunk, then fp64 in the lane's LDS slots (gcl)
   for (int blk = nblk - 1; ok && blk >= 0; --blk) {
     load_block(blk);
     kin = blk > 0 ? kbr + (long long)blk * (I + 1) : nullptr;
@@ -368,10 +365,10 @@ __device__ __forceinline__ void pde_adj_body(const PdeBwdArgs &p, double *ldsd) 
 #pragma unroll
     for (int r = 0; r < REP; ++r) rlast[r] = 1.0;
     rcorner = 1.0;
+    if constexpr (GCW > 0) {
 #pragma unroll
-    for (int w = 0; w < WC; ++w)
-#pragma unroll
-      for (int k = 0; k < DP; ++k) gcol[w][k] = 0.0;
+      for (int e = 0; e < GCW * DP; ++e) gcl[e * 64 + lane] = 0.0;
+    }
     const int nsteps = IC + U - 1;
     // the chunk's front, loaded one chunk ahead (the restore would otherwise wait on HBM at every chunk)
     float fv[FW];
@@ -397,10 +394,8 @@ __device__ __forceinline__ void pde_adj_body(const PdeBwdArgs &p, double *ldsd) 
         for (int k = 0; k < DPA; ++k) gcp[w2][k] = splat2(0.0f);
       // steps past nsteps touch no cell (ci >= IC in every lane used), and in the R sweep they come first,
       // on the boundary values 1: no guards
-      float dxc[H][DPA];
-      ldx_chunk(s0, dxc);
 #pragma unroll
-      for (int h = 0; h < H; ++h) kstep(s0 + h, dxc[h], kc[h], incH[h]);
+      for (int h = 0; h < H; ++h) kstep(s0 + h, kc[h], incH[h]);
 #pragma unroll
       for (int h = H - 1; h >= 0; --h) {
         double right[REP];
@@ -472,9 +467,10 @@ __device__ __forceinline__ void pde_adj_body(const PdeBwdArgs &p, double *ldsd) 
             for (int k = 0; k < DP; ++k)
               if (k < d) atomicAdd(gacc + ci * DP + k, (double)(gr[k][0] + gr[k][1]));
             if constexpr (COLS) {
+              const float *dxr = dxs + ci * DP;
 #pragma unroll
               for (int k = 0; k < DP; ++k) {
-                const f2 dxk = splat2(dxc[h][k]);
+                const f2 dxk = splat2(dxr[k]);
 #pragma unroll
                 for (int w2 = 0; w2 < WC2; ++w2) gcp[w2][k] = fma2(Sp[w2], dxk, gcp[w2][k]);
               }
@@ -483,11 +479,11 @@ __device__ __forceinline__ void pde_adj_body(const PdeBwdArgs &p, double *ldsd) 
         }
         rcorner = right[0];
       }
-      if constexpr (COLS && !TILE) {
+      if constexpr (GCW > 0) {
 #pragma unroll
         for (int w = 0; w < WC; ++w)
 #pragma unroll
-          for (int k = 0; k < DP; ++k) gcol[w][k] += (double)gcp[w / 2][k][w % 2];
+          for (int k = 0; k < DP; ++k) gcl[(w * DP + k) * 64 + lane] += (double)gcp[w / 2][k][w % 2];
       }
     }
     if constexpr (COLS && !TILE) {
@@ -502,7 +498,7 @@ __device__ __forceinline__ void pde_adj_body(const PdeBwdArgs &p, double *ldsd) 
 #pragma unroll
           for (int k = 0; k < DP; ++k) {  // compile-time indices: a runtime bound would put gcol in scratch
             if (k >= d) continue;
-            const float v = (float)(sy * gcol[w][k]);
+            const float v = (float)(sy * gcl[(w * DP + k) * 64 + lane]);
             unsafeAtomicAdd(gyb + (long long)(jc + 1) * d + k, v);
             unsafeAtomicAdd(gyb + (long long)jc * d + k, -v);
           }
@@ -538,10 +534,12 @@ static int launch_pde_adj(const PdeBwdArgs &a, long long nblocks, hipStream_t s)
   if constexpr (W < REP || REP * W > 64) {
     return GPSIG_EUNSUPPORTED;
   } else {
-    const size_t lds = DP == 0 ? 0 : (size_t)a.wpb * pde_lds_wave_doubles(a.l1 - 1, DP) * sizeof(double);
-    if (lds > 160 * 1024) return GPSIG_EUNSUPPORTED;
     // the column (dK/dy) accumulators only for cross pairs; k(x, x) takes twice the row part
-    if (a.pair_mode == GPSIG_PAIRS_DIAG || MODE == 1)
+    const bool cols = !(a.pair_mode == GPSIG_PAIRS_DIAG || MODE == 1);
+    const size_t lds =
+        DP == 0 ? 0 : (size_t)a.wpb * pde_lds_wave_doubles(a.l1 - 1, DP, cols ? W / REP : 0) * sizeof(double);
+    if (lds > 160 * 1024) return GPSIG_EUNSUPPORTED;
+    if (!cols)
       hipLaunchKernelGGL((pde_adj_kernel<DP, W, REP, false, MODE>), dim3((unsigned)nblocks), dim3(64 * a.wpb), lds, s, a);
     else
       hipLaunchKernelGGL((pde_adj_kernel<DP, W, REP, true, MODE>), dim3((unsigned)nblocks), dim3(64 * a.wpb), lds, s, a);

@@ -193,7 +193,9 @@ static int pde_adj_impl(int mode, const float *X, int n1, int l1, const float *Y
   // pairs per workgroup: 4 unless the per-wave LDS (row accumulators and dx of x) of long x needs fewer
   const int dp = d <= 8 ? d : (d <= 16 ? 16 : 0);
   int wpb = 4;
-  while (wpb > 1 && (size_t)wpb * pde_lds_wave_doubles(l1 - 1, dp) * sizeof(double) > 160 * 1024) wpb /= 2;
+  // cross pairs also keep their lanes' column sums in LDS (W / REP coarse columns per lane)
+  const int wc = pair_mode == GPSIG_PAIRS_RECT && mode != 1 ? pde_layout(l1, l2, dyadic).W >> dyadic : 0;
+  while (wpb > 1 && (size_t)wpb * pde_lds_wave_doubles(l1 - 1, dp, wc) * sizeof(double) > 160 * 1024) wpb /= 2;
   a.wpb = wpb;
   long long nblocks;
   if (pair_mode == GPSIG_PAIRS_DIAG) {
