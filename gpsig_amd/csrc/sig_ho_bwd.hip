@@ -53,6 +53,7 @@ static int ho_bwd_lds_launch(BwdArgs a, int o, int seed, hipStream_t s) {
     case 3: return sig_ho_bwd_lds_launch_o<3>(a, seed, nblocks, s);
     case 4: return sig_ho_bwd_lds_launch_o<4>(a, seed, nblocks, s);
     case 5: return sig_ho_bwd_lds_launch_o<5>(a, seed, nblocks, s);
+    case 6: return sig_ho_bwd_lds_launch_o<6>(a, seed, nblocks, s);
     default: return GPSIG_EUNSUPPORTED;
   }
 }

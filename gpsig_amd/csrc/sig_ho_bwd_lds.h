@@ -456,7 +456,7 @@ template <int ORD>
 int sig_ho_bwd_lds_launch_o(const BwdArgs &a, int seed, long long nblocks, hipStream_t s);
 
 // (effective order, levels, points) the LDS kernel covers: the multiplier slab of W = 4 / 8 columns fits
-constexpr int HO_LDS_MAX_ORD = 5;
+constexpr int HO_LDS_MAX_ORD = 6;  // order 6: 6 levels at up to 256 points (W = 4: 111 slab slots, 122 KB)
 inline bool ho_bwd_lds_fits(int o, int M, int l2) {
   int np = 0;
   for (int k = 1; k <= M; ++k) {

@@ -158,8 +158,8 @@ int gpsig_sig_gram_vjp(const float *X, int n1, int l1, const float *Y, int n2, i
 /* Gradient of the higher-order Gram (order > 1): TF autodiff of signature_kern_higher_order
  * (signature_algs.py:37-74) behind _K_seq / K.  Arguments as gpsig_sig_gram_vjp (difference = 1, no
  * saved state); order 1 forwards to it.  Supported: RBF / linear, any channel count, l2 <= 512, and
- * min(order, num_levels) <= 5 where the row state fits the LDS (l2 <= 256: order 2-4 to 8 levels,
- * order 5 to 7; l2 <= 512: order 2 to 8 levels, 3 to 7, 4 to 5, 5 at 5); otherwise
+ * min(order, num_levels) <= 6 where the row state fits the LDS (l2 <= 256: order 2-4 to 8 levels,
+ * order 5 to 7, order 6 at 6; l2 <= 512: order 2 to 8 levels, 3 to 7, 4 to 5, 5 at 5); otherwise
  * GPSIG_EUNSUPPORTED, and the workspace query returns 0. */
 size_t gpsig_sig_vjp_ho_workspace_bytes(int n1, int l1, int n2, int l2, int d, int num_levels, int order,
                                         int base_kind);

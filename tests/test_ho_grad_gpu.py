@@ -81,11 +81,11 @@ def test_higher_order_diag_and_norms_gradient():
 
 
 def test_unsupported_higher_order_gradients_raise():
-    """Orders past the VJP kernels (min(order, num_levels) = 6 here) that are not the exact linear kernel
-    evaluate forward; their backward raises."""
+    """Orders past the VJP kernels (min(order, num_levels) = 7; order 6 at 7 levels, whose slab does not fit the
+    LDS) that are not the exact linear kernel evaluate forward; their backward raises."""
     import gpsig_amd
     X = torch.tensor(golden("linear_chen.npz")["X"][:4].reshape(4, -1), device=DEV, requires_grad=True)
-    for k in (gpsig_amd.SignatureRBF(60, 3, 6, order=6), gpsig_amd.SignatureLinear(60, 3, 7, order=6)):
+    for k in (gpsig_amd.SignatureRBF(60, 3, 7, order=7), gpsig_amd.SignatureLinear(60, 3, 7, order=6)):
         K = k.K(X)
         with pytest.raises(NotImplementedError):
             K.sum().backward()
@@ -103,6 +103,8 @@ def _walks(n, l, d, seed):
     (19, 4, 4, 4, "linear"), (300, 3, 4, 2, "rbf"), (270, 2, 5, 5, "linear"), (400, 3, 5, 4, "rbf"),
     # 257-509 points: one pair over the 4 SIMDs of a CU (csrc/sig_ho_bwd_split.h), 3 and 4 column blocks
     (381, 3, 4, 3, "rbf"), (509, 2, 3, 2, "linear"),
+    # effective order 6 (6 levels, up to 256 points: the LDS-state kernel at W = 4)
+    (20, 3, 6, 6, "rbf"), (18, 2, 6, 7, "rbf"), (200, 2, 6, 6, "linear"),
 ])
 def test_higher_order_vjp_kernel_raw_levels(L, D, M, order, base):
     """gpsig_sig_gram_vjp_ho (csrc/sig_ho_bwd.h, sig_ho_bwd_lds.h) against fp64 autodiff of
@@ -163,12 +165,12 @@ def test_higher_order_normalised_K_gradient(cross, base):
 
 
 def test_higher_order_vjp_unsupported_raises():
-    """min(order, M) = 6, sequences past 512 points, and (order, levels) whose multiplier slab does not fit
-    the LDS at 257-512 points are outside the VJP kernels: the error names the entry point (autograd then
-    uses the signature-feature path for the exact linear kernel, or raises)."""
+    """min(order, M) = 7, order 6 at 7 levels or past 256 points, sequences past 512 points, and (order, levels)
+    whose multiplier slab does not fit the LDS at 257-512 points are outside the VJP kernels: the error names the
+    entry point (autograd then uses the signature-feature path for the exact linear kernel, or raises)."""
     from gpsig_amd import _lib as Lb
     from gpsig_amd import ops
-    for L, M, order in ((10, 6, 6), (600, 3, 2), (300, 6, 4), (300, 8, 3)):
+    for L, M, order in ((10, 7, 7), (10, 7, 6), (300, 6, 6), (600, 3, 2), (300, 6, 4), (300, 8, 3)):
         X = torch.zeros((2, L, 2), device=DEV)
         with pytest.raises(Lb.GpsigError):
             ops.sig_gram_vjp(X, None, M, torch.zeros((M + 1, 2, 2), device=DEV), gout_levels=True, order=order)
