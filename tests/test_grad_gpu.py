@@ -191,11 +191,11 @@ def test_raw_levels_vjp_no_difference_ragged(base):
 
 
 def test_higher_order_backward_raises():
-    """min(order, num_levels) = 6 with the RBF base kernel: outside the higher-order VJP kernels (orders
-    2-5, tests/test_ho_grad_gpu.py) and not the exact signature kernel -> NotImplementedError."""
+    """min(order, num_levels) = 7 with the RBF base kernel: outside the higher-order VJP kernels (orders
+    2-5, and 6 at 6 levels, tests/test_ho_grad_gpu.py) and not the exact signature kernel -> NotImplementedError."""
     import gpsig_amd
     X = walks(4, 10, 2, 0)
-    k = gpsig_amd.SignatureRBF(20, 2, 6, order=6)
+    k = gpsig_amd.SignatureRBF(20, 2, 7, order=7)
     Xt = torch.tensor(X.reshape(4, -1), device=DEV, requires_grad=True)
     with pytest.raises(NotImplementedError):
         k.K(Xt).sum().backward()
