@@ -205,15 +205,16 @@ __global__ __launch_bounds__(64 * HO_SPLIT_NW) __attribute__((amdgpu_waves_per_e
   };
   // this wave's part of the multiplier slab: slot s of this lane's W columns
   float *__restrict__ ps = pslab + (long long)wave * (Lay::np + Lay::ncb) * 64 * W + lane * W;
+  // no compiler barriers around the slab accesses here (the one-wave kernel needs them to bound its register
+  // use at W = 8): each lane touches only its own columns, so the compiler may batch a level's LDS reads
+  // ahead of their use instead of paying each read's latency in turn
   auto pget = [&](int slot, float (&v)[W]) {
-    asm volatile("" ::: "memory");
     const f2 t = *reinterpret_cast<const f2 *>(ps + (long long)slot * 64 * W);
     v[0] = t[0];
     v[1] = t[1];
   };
   auto pput = [&](int slot, const float (&v)[W]) {
     *reinterpret_cast<f2 *>(ps + (long long)slot * 64 * W) = (f2){v[0], v[1]};
-    asm volatile("" ::: "memory");
   };
   constexpr int CBS = Lay::np;
   auto cadd = [&](int k, const float (&v)[W], float sgn) {
