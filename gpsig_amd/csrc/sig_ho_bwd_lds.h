@@ -31,6 +31,9 @@ constexpr size_t ho_bwd_lds_slab_bytes() {
 }
 constexpr size_t ho_bwd_lds_cbuf_bytes(int W) { return (size_t)GPSIG_WIDE_BWD_R * 64 * 2 * W * sizeof(float); }
 
+#ifndef HO_LDS_NOFENCE_SLOTS
+#define HO_LDS_NOFENCE_SLOTS 100  // 99 slots (order 5 at 6 levels, 4 at 7) run unfenced without spills; 111 (order 6) spill
+#endif
 template <int ORD, int M, int W, int SEED>
 __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void sig_ho_bwd_lds_kernel(BwdArgs p) {
   constexpr int W2 = W / 2;
@@ -129,8 +132,12 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void si
   };
   // the multiplier slab: slot s of this lane's W columns
   float *__restrict__ ps = pslab + lane * W;
+  // Compiler barriers around the slab accesses bound the register use where the slab is large (W = 8, or many
+  // slots): without them a level's reads are hoisted and the kernel spills (W = 4 at 7 levels).  Small slabs
+  // go without: the reads of a level batch ahead of their use (each lane touches only its own columns).
+  constexpr bool FENCE = W > 4 || Lay::np + Lay::ncb > HO_LDS_NOFENCE_SLOTS;
   auto pget = [&](int slot, float (&v)[W]) {
-    asm volatile("" ::: "memory");
+    if constexpr (FENCE) asm volatile("" ::: "memory");
 #pragma unroll
     for (int h = 0; h < W / 4; ++h) {
       const f4 t = *reinterpret_cast<const f4 *>(ps + (long long)slot * 64 * W + 4 * h);
@@ -142,7 +149,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void si
 #pragma unroll
     for (int h = 0; h < W / 4; ++h)
       *reinterpret_cast<f4 *>(ps + (long long)slot * 64 * W + 4 * h) = (f4){v[4 * h], v[4 * h + 1], v[4 * h + 2], v[4 * h + 3]};
-    asm volatile("" ::: "memory");
+    if constexpr (FENCE) asm volatile("" ::: "memory");
   };
   // the column sums CB_m[y] follow the multipliers in the slab
   constexpr int CBS = Lay::np;
