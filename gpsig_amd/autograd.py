@@ -20,7 +20,8 @@ exceed it saves nothing and its backward recomputes.
 Gradients reach the sequences (and, through the host-side scaling in kernels.py, the lengthscales)
 and sigma * variances.  Supported for order == 1 (difference True or False); for order > 1 the Gram and
 its diagonal through gpsig_sig_gram_vjp_ho (csrc/sig_ho_bwd.h, sig_ho_bwd_lds.h: min(order, M) = 2..5,
-lengths <= 512, and 6 at 6 levels up to 256 points, where the row state fits the LDS)
+lengths <= 512, and 6 at 6 levels up to 256 points, where the row state fits the LDS; up to 1017 points at
+orders 2-5 with a global-memory slab)
 and, beyond it, for SignatureLinear with order >= num_levels (the exact signature kernel; backward
 through the signature features, ops.sig_gram_ho_vjp); other higher orders evaluate forward but raise
 NotImplementedError on backward.  The RBF higher order past 32 channels takes its cells from the matrix-core
@@ -91,8 +92,8 @@ def _check_bwd(cfg, gram=False):
     if cfg["order"] != 1 and not (gram and _ho_signature_case(cfg)):
         raise NotImplementedError("gradients of the signature kernels are implemented for order=1 "
                                   "(gpsig_sig_gram_vjp, gpsig_tens_vs_seq_vjp), for the Gram and its diagonal "
-                                  "at min(order, num_levels) in 2..5 up to length 512 and 6 at 6 levels up to 256 "
-                                  "(gpsig_sig_gram_vjp_ho), "
+                                  "at min(order, num_levels) in 2..5 up to length 512 (1017 at fewer levels) and 6 at 6 "
+                                  "levels up to 256 (gpsig_sig_gram_vjp_ho), "
                                   "and for SignatureLinear with order >= num_levels")
 
 

@@ -9,6 +9,7 @@ size_t sig_bwd_wide_workspace(int n1, int l1, int n2, int l2, int d);
 int sig_bwd_wide(BwdArgs a, const float *X, const float *Y, int seed, void *workspace, size_t workspace_bytes,
                  hipStream_t s, int order = 1);
 bool ho_bwd_supported(int l2, int order, int M, int seed);
+size_t ho_bwd_slab_bytes(int l2, int order, int M);
 // channel counts past the VJP's instantiations: the wide-channel VJP (point-weight tiles + GEMMs; slower
 // than the register form at few channels: d = 5 69.7 vs 31.8 ms fwd+bwd at N = 1024, L = 100).
 // GPSIG_VJP_FIXED_MAX lowers the crossover for A/B runs.
@@ -91,8 +92,13 @@ static int tile_vjp(const float *X, int n1, int l1, const float *Y, int n2, int 
     a.gscale = gsc_slots;
   }
   a.state = state;
+  // the 8-wave higher-order VJP's global slabs (past 509 points) after the wide workspace
+  const size_t wide_b = sig_bwd_wide_workspace(n1, l1, n2, l2, d);
+  const size_t slab_b = order > 1 ? ho_bwd_slab_bytes(l2, order, num_levels) : 0;
+  if (workspace_bytes < GSC_BYTES + wide_b + slab_b) return GPSIG_EWORKSPACE;
+  a.scratch = slab_b ? reinterpret_cast<float *>(static_cast<char *>(workspace) + GSC_BYTES + wide_b) : nullptr;
   const int rc = sig_bwd_wide(a, X, pair_mode == GPSIG_PAIRS_RECT ? Y : X, seed, static_cast<char *>(workspace) + GSC_BYTES,
-                              workspace_bytes - GSC_BYTES, s, order);
+                              wide_b, s, order);
   if (rc) return rc;
   if (a.gscale) {
     hipLaunchKernelGGL(gscale_reduce_kernel, dim3(1), dim3(64), 0, s, gsc_slots, num_levels + 1, gscale);
@@ -258,5 +264,5 @@ extern "C" size_t gpsig_sig_vjp_ho_workspace_bytes(int n1, int l1, int n2, int l
   if (order == 1 || num_levels == 1) return gpsig_sig_vjp_workspace_bytes(n1, l1, n2, l2, d, num_levels, 1);
   const int seed = base_kind == GPSIG_BASE_RBF ? SEED_RBF_DIFF : base_kind == GPSIG_BASE_LINEAR ? SEED_LIN_DIFF : -1;
   if (seed < 0 || !ho_bwd_supported(l2, order, num_levels, seed)) return 0;
-  return GSC_BYTES + sig_bwd_wide_workspace(n1, l1, n2, l2, d);
+  return GSC_BYTES + sig_bwd_wide_workspace(n1, l1, n2, l2, d) + ho_bwd_slab_bytes(l2, order, num_levels);
 }

@@ -203,7 +203,7 @@ int sig_bwd_wide(BwdArgs a, const float *X, const float *Y, int seed, void *work
   a.sy = wide_rec_floats(d, l2);
   a.tile = T;
   a.nblk = 1;
-  a.scratch = nullptr;
+  if (order == 1) a.scratch = nullptr;  // order > 1: the caller's slab region of the 8-wave split VJP (or null)
   a.scr_stride = 0;
   const int G = 64 / geo.LP;
   const int ntb = (n2 + G - 1) / G;

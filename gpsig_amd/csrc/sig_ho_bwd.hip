@@ -1,7 +1,7 @@
 // gpsig_amd -- launches of the higher-order Gram VJP kernel (sig_ho_bwd.h): orders 2 (levels 2..8) and 3
 // (levels 3..5), the (order, levels) whose multiplier slab fits the LDS next to the cell buffer.  Orders
 // at or above the level count are the exact signature kernel: order min(order, M).
-#include "sig_ho_bwd_lds.h"
+#include "sig_ho_bwd_split.h"
 
 namespace gpsig {
 
@@ -27,9 +27,17 @@ static bool ho_bwd_reg(int l2, int o, int M) { return l2 <= 256 && (o == 2 || (o
 
 bool ho_bwd_supported(int l2, int order, int M, int seed) {
   if (seed != SEED_RBF_DIFF && seed != SEED_LIN_DIFF) return false;
-  if (l2 < 2 || l2 > 512 || M < 2 || M > 8 || order < 2) return false;
+  if (l2 < 2 || M < 2 || M > 8 || order < 2) return false;
   const int o = ho_eff_order(order, M);
+  if (l2 > HO_SPLIT_NW * HO_SPLIT_CPB + 1) return o <= HO_LDS_MAX_ORD && ho_bwd_split8_fits(o, M, l2);
   return ho_bwd_reg(l2, o, M) || (o <= HO_LDS_MAX_ORD && ho_bwd_lds_fits(o, M, l2));
+}
+
+// global slabs of the 8-wave split VJP (510 .. 1017 points): one launch chunk of workgroups
+size_t ho_bwd_slab_bytes(int l2, int order, int M) {
+  const int o = ho_eff_order(order, M);
+  if (!ho_bwd_split8_fits(o, M, l2)) return 0;
+  return (size_t)HO_SPLIT8_BLOCKS * (size_t)ho_split_slab_floats_rt(o, M, HO_SPLIT8_NW) * sizeof(float);
 }
 
 // The LDS kernel runs one pair per workgroup: its own grid over the launch's rows [row_begin, row_end)

@@ -22,6 +22,29 @@ constexpr int HO_SPLIT_NW = 4;                                // waves (column b
 constexpr int HO_SPLIT_W = 2;                                 // columns per lane
 constexpr int HO_SPLIT_CPB = 64 * HO_SPLIT_W - 1;             // cells per block
 constexpr int HO_SPLIT_XN = 8;                                // values per wave and exchange (>= max order)
+// Past 4 blocks (510 .. 8 x 127 + 1 points): NW = 8 waves, 2 per SIMD, and the slab (twice the LDS) in a
+// per-workgroup region of global memory (BwdArgs::scratch, scr_stride floats per workgroup: L2-resident per
+// CU); launches are split into at most HO_SPLIT8_BLOCKS workgroups (blk0) to bound that region.
+constexpr int HO_SPLIT8_NW = 8;
+constexpr long long HO_SPLIT8_BLOCKS = 1024;
+template <int ORD, int M>
+constexpr long long ho_split_slab_floats(int nw) {
+  return (long long)nw * (HoBwdLayout<ORD, M>::np + HoBwdLayout<ORD, M>::ncb) * 64 * HO_SPLIT_W;
+}
+inline long long ho_split_slab_floats_rt(int o, int M, int nw) {
+  int np = 0;
+  for (int k = 1; k <= M; ++k) {
+    const int d = k < o ? k : o;
+    np += (k >= 2 ? d * d : 0) + d;
+  }
+  return (long long)nw * np * 64 * HO_SPLIT_W;
+}
+// the 8-wave form covers 510 .. 1017 points where its per-lane state fits 256 VGPRs (2 waves per SIMD) without
+// spilling: levels up to 7 / 6 / 5 / 5 at effective order 2 / 3 / 4 / 5 (order 5 with the RBF seed: 20 bytes)
+constexpr bool ho_split8_ok(int o, int M) { return (o == 2 && M <= 7) || (o == 3 && M <= 6) || ((o == 4 || o == 5) && M <= 5); }
+inline bool ho_bwd_split8_fits(int o, int M, int l2) {
+  return l2 > HO_SPLIT_NW * HO_SPLIT_CPB + 1 && l2 <= HO_SPLIT8_NW * HO_SPLIT_CPB + 1 && ho_split8_ok(o, M);
+}
 
 // (effective order, levels, points) the split kernel covers: 257 .. 4 x 127 + 1 points (wide records padded
 // to 512 columns, so every block's 128 columns lie in the record) and the slab of W = 8 fits
@@ -39,10 +62,11 @@ constexpr size_t ho_bwd_split_slab_bytes() {
   return (size_t)HO_SPLIT_NW * (ho_lds_np<ORD, M>() + HoBwdLayout<ORD, M>::ncb) * 64 * HO_SPLIT_W * sizeof(float);
 }
 
-template <int ORD, int M, int SEED>
-__global__ __launch_bounds__(64 * HO_SPLIT_NW) __attribute__((amdgpu_waves_per_eu(1))) void sig_ho_bwd_split_kernel(
+template <int ORD, int M, int SEED, int NW = HO_SPLIT_NW>
+__global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4))) void sig_ho_bwd_split_kernel(
     BwdArgs p) {
-  constexpr int NW = HO_SPLIT_NW, W = HO_SPLIT_W, W2 = W / 2, CPB = HO_SPLIT_CPB, XN = HO_SPLIT_XN;
+  constexpr int W = HO_SPLIT_W, W2 = W / 2, CPB = HO_SPLIT_CPB, XN = HO_SPLIT_XN;
+  constexpr bool GLB = NW > HO_SPLIT_NW;  // the slab in global memory
   constexpr int RC = GPSIG_WIDE_BWD_R;
   constexpr bool RBF = SEED == SEED_RBF_DIFF;
   static_assert(SEED == SEED_RBF_DIFF || SEED == SEED_LIN_DIFF, "higher order: difference seeds");
@@ -111,20 +135,20 @@ __global__ __launch_bounds__(64 * HO_SPLIT_NW) __attribute__((amdgpu_waves_per_e
     ptv[w] = j0 + jj < l2 && (jj < CPB || wave == NW - 1);  // a block's halo point is the next block's first
   }
 
-  // cross-block exchange: N per-wave values (uniform in the wave) -> every wave's values; one barrier
+  // cross-block exchange: N per-wave values (uniform in the wave) -> every wave's values; one barrier.  The
+  // values stay in LDS (broadcast reads, xget) rather than NW x N registers.
   int ph = 0;
-  auto exchange = [&](auto nt, const float *mine, float (*all)[XN]) {
+  auto exchange = [&](auto nt, const float *mine) {
     constexpr int N = decltype(nt)::value;
     if (lane == 0)
 #pragma unroll
       for (int n = 0; n < N; ++n) xbuf[ph][wave][n] = mine[n];
     __syncthreads();
-#pragma unroll
-    for (int u = 0; u < NW; ++u)
-#pragma unroll
-      for (int n = 0; n < N; ++n) all[u][n] = xbuf[ph][u][n];
+    const int cur = ph;
     ph ^= 1;
+    return cur;
   };
+  auto xget = [&](int buf, int u, int n) { return xbuf[buf][u][n]; };
   // exclusive (REV: reverse exclusive) scans over the pair's columns of N arrays: in-lane, over the wave, then
   // the totals of the blocks to the left (right)
   auto scan_cols = [&](auto nt, auto rev, const float (*v)[W], float (*out)[W]) {
@@ -142,14 +166,13 @@ __global__ __launch_bounds__(64 * HO_SPLIT_NW) __attribute__((amdgpu_waves_per_e
     group_incl_scan_n<64, N>(incl);
 #pragma unroll
     for (int n = 0; n < N; ++n) tot[n] = __shfl(incl[n], 63, 64);
-    float all[NW][XN];
-    exchange(nt, tot, all);
+    const int xb = exchange(nt, tot);
 #pragma unroll
     for (int n = 0; n < N; ++n) {
       float off = 0.0f;
 #pragma unroll
       for (int u = 0; u < NW; ++u)
-        if (REV ? u > wave : u < wave) off += all[u][n];
+        if (REV ? u > wave : u < wave) off += xget(xb, u, n);
       if constexpr (!REV) {
         float run = off + (incl[n] - t[n]);
 #pragma unroll
@@ -204,17 +227,22 @@ __global__ __launch_bounds__(64 * HO_SPLIT_NW) __attribute__((amdgpu_waves_per_e
     for (int w = 0; w < W; ++w) asm volatile("" : "+v"(v[w]));
   };
   // this wave's part of the multiplier slab: slot s of this lane's W columns
-  float *__restrict__ ps = pslab + (long long)wave * (Lay::np + Lay::ncb) * 64 * W + lane * W;
+  float *__restrict__ slab = GLB ? p.scratch + (long long)blockIdx.x * p.scr_stride : pslab;
+  float *__restrict__ ps = slab + (long long)wave * (Lay::np + Lay::ncb) * 64 * W + lane * W;
   // no compiler barriers around the slab accesses here (the one-wave kernel needs them to bound its register
   // use at W = 8): each lane touches only its own columns, so the compiler may batch a level's LDS reads
   // ahead of their use instead of paying each read's latency in turn
+  // (the 8-wave form, 2 waves per SIMD at <= 256 VGPRs, keeps the barriers: unfenced, its global slab reads are
+  // hoisted past the register file)
   auto pget = [&](int slot, float (&v)[W]) {
+    if constexpr (GLB) asm volatile("" ::: "memory");
     const f2 t = *reinterpret_cast<const f2 *>(ps + (long long)slot * 64 * W);
     v[0] = t[0];
     v[1] = t[1];
   };
   auto pput = [&](int slot, const float (&v)[W]) {
     *reinterpret_cast<f2 *>(ps + (long long)slot * 64 * W) = (f2){v[0], v[1]};
+    if constexpr (GLB) asm volatile("" ::: "memory");
   };
   constexpr int CBS = Lay::np;
   auto cadd = [&](int k, const float (&v)[W], float sgn) {
@@ -329,13 +357,12 @@ __global__ __launch_bounds__(64 * HO_SPLIT_NW) __attribute__((amdgpu_waves_per_e
       ks[(m - 1) % XN] = group_sum<64>(s);
       if constexpr (m % XN == 0 || m == M) {  // the blocks' sums, XN levels per exchange
         constexpr int n0 = ((m - 1) / XN) * XN, cnt = m - n0;
-        float all[NW][XN];
-        exchange(std::integral_constant<int, cnt>{}, ks, all);
+        const int xb = exchange(std::integral_constant<int, cnt>{}, ks);
 #pragma unroll
         for (int n = 0; n < cnt; ++n) {
           float t = 0.0f;
 #pragma unroll
-          for (int u = 0; u < NW; ++u) t += all[u][n];
+          for (int u = 0; u < NW; ++u) t += xget(xb, u, n);
           K[n0 + n + 1] = t;
         }
       }
@@ -483,10 +510,9 @@ __global__ __launch_bounds__(64 * HO_SPLIT_NW) __attribute__((amdgpu_waves_per_e
     // adjoint of the second difference (signature_algs.py:26): E(i, j) = Dh(i, j-1) - Dh(i, j); at the block's
     // first point Dh(i, j0 - 1) is the left block's last cell (lane 63, column 0)
     float mine[1] = {__shfl(Dh[0], 63, 64)};
-    float all[NW][XN];
-    exchange(std::integral_constant<int, 1>{}, mine, all);
+    const int xb = exchange(std::integral_constant<int, 1>{}, mine);
     float left = lane_prev(Dh[W - 1]);
-    if (lane == 0) left = wave > 0 ? all[wave > 0 ? wave - 1 : 0][0] : 0.0f;
+    if (lane == 0) left = wave > 0 ? xget(xb, wave > 0 ? wave - 1 : 0, 0) : 0.0f;
     float Kh[W];
 #pragma unroll
     for (int w = 0; w < W; ++w) {

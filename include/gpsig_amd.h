@@ -159,8 +159,9 @@ int gpsig_sig_gram_vjp(const float *X, int n1, int l1, const float *Y, int n2, i
  * (signature_algs.py:37-74) behind _K_seq / K.  Arguments as gpsig_sig_gram_vjp (difference = 1, no
  * saved state); order 1 forwards to it.  Supported: RBF / linear, any channel count, l2 <= 512, and
  * min(order, num_levels) <= 6 where the row state fits the LDS (l2 <= 256: order 2-4 to 8 levels,
- * order 5 to 7, order 6 at 6; l2 <= 512: order 2 to 8 levels, 3 to 7, 4 to 5, 5 at 5); otherwise
- * GPSIG_EUNSUPPORTED, and the workspace query returns 0. */
+ * order 5 to 7, order 6 at 6; l2 <= 512: order 2 to 8 levels, 3 to 7, 4 to 5, 5 at 5), and 510 <= l2 <= 1017
+ * at order 2 to 7 levels, 3 to 6, 4 and 5 to 5 (8 waves per pair, the multiplier slabs in the workspace: the
+ * workspace query includes them); otherwise GPSIG_EUNSUPPORTED, and the workspace query returns 0. */
 size_t gpsig_sig_vjp_ho_workspace_bytes(int n1, int l1, int n2, int l2, int d, int num_levels, int order,
                                         int base_kind);
 int gpsig_sig_gram_vjp_ho(const float *X, int n1, int l1, const float *Y, int n2, int l2, int d, int num_levels,

@@ -165,12 +165,14 @@ def test_higher_order_normalised_K_gradient(cross, base):
 
 
 def test_higher_order_vjp_unsupported_raises():
-    """min(order, M) = 7, order 6 at 7 levels or past 256 points, sequences past 512 points, and (order, levels)
-    whose multiplier slab does not fit the LDS at 257-512 points are outside the VJP kernels: the error names the
-    entry point (autograd then uses the signature-feature path for the exact linear kernel, or raises)."""
+    """min(order, M) = 7, order 6 at 7 levels or past 256 points, sequences past 1017 points, (order, levels)
+    whose multiplier slab does not fit the LDS at 257-509 points or whose state does not fit the 8-wave form past
+    509 are outside the VJP kernels: the error names the entry point (autograd then uses the signature-feature
+    path for the exact linear kernel, or raises)."""
     from gpsig_amd import _lib as Lb
     from gpsig_amd import ops
-    for L, M, order in ((10, 7, 7), (10, 7, 6), (300, 6, 6), (600, 3, 2), (300, 6, 4), (300, 8, 3)):
+    for L, M, order in ((10, 7, 7), (10, 7, 6), (300, 6, 6), (1100, 3, 2), (700, 8, 2), (600, 6, 4), (300, 6, 4),
+                        (300, 8, 3)):
         X = torch.zeros((2, L, 2), device=DEV)
         with pytest.raises(Lb.GpsigError):
             ops.sig_gram_vjp(X, None, M, torch.zeros((M + 1, 2, 2), device=DEV), gout_levels=True, order=order)
@@ -302,3 +304,29 @@ def test_higher_order_vjp_split_matches_one_wave_kernel(L, M, order, base, monke
     one = grads()
     for g, r in zip(split, one):
         assert norm_rel_err(g, r) < 2e-6
+
+
+@pytest.mark.parametrize("L,D,M,order,base", [(700, 3, 4, 3, "rbf"), (1017, 2, 3, 2, "linear"), (600, 3, 5, 5, "rbf"),
+                                               (510, 2, 5, 4, "linear")])
+def test_higher_order_vjp_past_512_points(L, D, M, order, base):
+    """510-1017 points: one pair over 8 waves (2 per SIMD), the multiplier slab in a global-memory region of the
+    workspace (csrc/sig_ho_bwd_split.h, NW = 8), against fp64 autodiff of signature_kern_higher_order on cross,
+    symmetric and diagonal pairs."""
+    from gpsig_amd import ops
+    X, Y = _walks(2, L, D, L + order), _walks(2, L - 5, D, L + order + 1)
+    G = np.random.default_rng(7).standard_normal((M + 1, 2, 2))
+    Gd = np.random.default_rng(9).standard_normal((M + 1, 2))
+    Xt, Yt = torch.tensor(X, device=DEV, dtype=torch.float32), torch.tensor(Y, device=DEV, dtype=torch.float32)
+    gX, gY = ops.sig_gram_vjp(Xt, Yt, M, torch.tensor(G, device=DEV), base=base, gout_levels=True, order=order)
+    Xr, Yr = torch.tensor(X, requires_grad=True), torch.tensor(Y, requires_grad=True)
+    (ar.k_seq(Xr, Yr, M, base, order=order) * torch.tensor(G)).sum().backward()
+    assert norm_rel_err(gX.cpu().numpy(), Xr.grad.numpy()) < GTOL
+    assert norm_rel_err(gY.cpu().numpy(), Yr.grad.numpy()) < GTOL
+    gS, _ = ops.sig_gram_vjp(Xt, None, M, torch.tensor(G, device=DEV), base=base, gout_levels=True, order=order)
+    Xr = torch.tensor(X, requires_grad=True)
+    (ar.k_seq(Xr, Xr, M, base, order=order) * torch.tensor(G)).sum().backward()
+    assert norm_rel_err(gS.cpu().numpy(), Xr.grad.numpy()) < GTOL
+    gD, _ = ops.sig_gram_vjp(Xt, None, M, torch.tensor(Gd, device=DEV), base=base, diag=True, order=order)
+    Xr = torch.tensor(X, requires_grad=True)
+    (ar.k_seq_diag(Xr, M, base, order=order) * torch.tensor(Gd)).sum().backward()
+    assert norm_rel_err(gD.cpu().numpy(), Xr.grad.numpy()) < GTOL
