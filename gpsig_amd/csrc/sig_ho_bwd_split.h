@@ -171,8 +171,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4)
     for (int n = 0; n < N; ++n) {
       float off = 0.0f;
 #pragma unroll
-      for (int u = 0; u < NW; ++u)
-        if (REV ? u > wave : u < wave) off += xget(xb, u, n);
+      for (int u = 0; u < NW; ++u) {  // unconditional reads (batched after the barrier), predicated adds
+        const float t = xget(xb, u, n);
+        off += (REV ? u > wave : u < wave) ? t : 0.0f;
+      }
       if constexpr (!REV) {
         float run = off + (incl[n] - t[n]);
 #pragma unroll
