@@ -25,6 +25,7 @@
 //     e_ij = -|x_i - y_j|^2 / 2,  e_{i+1,j} = e_ij + p_ij,  e_{0,j+1} = e_0j + q_0j   (e_00 exact)
 // k = exp(e) and expm1(q) by the exp-free recurrences between anchor rows, re-anchored from e and Q.
 #pragma once
+#include <stdlib.h>
 #include "sig_common.h"
 
 namespace gpsig {
@@ -69,7 +70,8 @@ inline size_t mf_lds_bytes(int d, int l2, int nw) {
 // the LDS allows, else 4 (wide B images: d > 114 at 129..160 points); 0: no tile geometry
 inline int mf_waves(int d, int l2) {
   if (mf_w(l2) == 0) return 0;
-  if (mf_lds_bytes(d, l2, 8) <= MF_LDS_MAX) return 8;
+  static const bool four = [] { const char *e = getenv("GPSIG_MF_NW"); return e && e[0] == '4'; }();  // A/B
+  if (!four && mf_lds_bytes(d, l2, 8) <= MF_LDS_MAX) return 8;
   return mf_lds_bytes(d, l2, 4) <= MF_LDS_MAX ? 4 : 0;
 }
 inline bool mf_applies(int d, int l2) { return mf_waves(d, l2) != 0; }
