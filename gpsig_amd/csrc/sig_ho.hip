@@ -212,15 +212,17 @@ __global__ __launch_bounds__(256) void sig_ho_kernel(SigArgs p) {
               if (x < dn)
 #pragma unroll
                 for (int w = 0; w < W; ++w) in[x][w] = x == 0 ? tot[w] : rowsum[x - 1][w];
+            // the level's scans step-interleaved (one DPP chain per value would wait on each step's result)
 #pragma unroll
-            for (int x = 0; x < ORD; ++x)
-              if (x < dn) {
-                float c = 0.0f;
+            for (int x = 0; x < ORD; ++x) {
+              float c = 0.0f;
+              if (x < dn)
 #pragma unroll
                 for (int w = 0; w < W; ++w) c += in[x][w];
-                t[x] = c;
-                incl[x] = group_incl_scan<64>(c);
-              }
+              t[x] = c;
+              incl[x] = c;
+            }
+            group_incl_scan_n<64, ORD>(incl);
             if (lane == 63)
 #pragma unroll
               for (int x = 0; x < ORD; ++x)
@@ -231,8 +233,10 @@ __global__ __launch_bounds__(256) void sig_ho_kernel(SigArgs p) {
               if (x < dn) {
                 float base = incl[x] - t[x];
 #pragma unroll
-                for (int u = 0; u < 4; ++u)
-                  if (u < wave) base += hx[ph][u][x];
+                for (int u = 0; u < 4; ++u) {  // unconditional reads (batched after the barrier), predicated adds
+                  const float h = hx[ph][u][x];
+                  base += u < wave ? h : 0.0f;
+                }
                 float *o = x == 0 ? S00 : Sa[x];
                 o[0] = base;
 #pragma unroll
