@@ -244,10 +244,35 @@ __global__ __launch_bounds__(256) void sig_ho_kernel(SigArgs p) {
               }
             ph ^= 1;
           } else {
-            excl_scan_cols<W>(tot, S00, cr + Lay::coff(m), blk, nblk);
+            // the level's dn exclusive column scans, their DPP steps interleaved (in-lane totals first; the
+            // in-lane prefixes are rebuilt when the outputs are written)
+            float c[ORD], incl[ORD];
 #pragma unroll
-            for (int x = 1; x < ORD; ++x)
-              if (x < dn) excl_scan_cols<W>(rowsum[x - 1], Sa[x], cr + Lay::coff(m) + x, blk, nblk);
+            for (int x = 0; x < ORD; ++x) {
+              float t = 0.0f;
+              if (x < dn)
+#pragma unroll
+                for (int w = 0; w < W; ++w) t += x == 0 ? tot[w] : rowsum[x > 0 ? x - 1 : 0][w];
+              c[x] = t;
+              incl[x] = t;
+            }
+            group_incl_scan_n<64, ORD>(incl);
+#pragma unroll
+            for (int x = 0; x < ORD; ++x)
+              if (x < dn) {
+                float base = incl[x] - c[x];
+                if (nblk > 1) {  // wave-uniform: the carry of the blocks to the left, this block's total onwards
+                  float *crx = cr + Lay::coff(m) + x;
+                  const float cin = blk > 0 ? *crx : 0.0f;
+                  const float bt = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, incl[x]), 63));
+                  if (blk + 1 < nblk && lane == 0) *crx = cin + bt;
+                  base += cin;
+                }
+                float *o = x == 0 ? S00 : Sa[x];
+                o[0] = base;
+#pragma unroll
+                for (int w = 1; w < W; ++w) o[w] = o[w - 1] + (x == 0 ? tot[w - 1] : rowsum[x > 0 ? x - 1 : 0][w - 1]);
+              }
           }
           // new blocks, in place: same-cell chain first (descending), then the edges
 #pragma unroll
