@@ -17,6 +17,12 @@
 
 namespace gpsig {
 
+// 1 / k!, k = 0..16: the exponential's and Chen's coefficients as multiplications (a division per term is a
+// ten-instruction sequence); indexed by wave-uniform level counts, so read through the scalar cache
+__constant__ float c_invfact[17] = {1.0f, 1.0f, 0.5f, 1.6666667e-1f, 4.1666668e-2f, 8.3333338e-3f, 1.3888889e-3f,
+                                    1.9841270e-4f, 2.4801587e-5f, 2.7557319e-6f, 2.7557319e-7f, 2.5052108e-8f,
+                                    2.0876757e-9f, 1.6059044e-10f, 1.1470746e-11f, 7.6471637e-13f, 4.7794773e-14f};
+
 struct SigFeatArgs {
   const float *X;  // (n, l, d)
   int n, l, d, depth;
@@ -54,22 +60,26 @@ __global__ __launch_bounds__(256) void sig_features_kernel(SigFeatArgs a) {
   }
   const float *x = a.X + (long long)path * a.l * d;
   const DivD dv(d);
+  // (tid < d) the path's points: x_s kept from the previous step, x_{s+1} loaded one step ahead
+  float xc = tid < d ? x[tid] : 0.0f, xn = tid < d && a.l > 1 ? x[d + tid] : 0.0f;
   for (int s = 0; s + 1 < a.l; ++s) {
+    const float xnn = tid < d && s + 2 < a.l ? x[(s + 2) * d + tid] : 0.0f;
     __syncthreads();
-    if (tid < d) h[tid] = x[(s + 1) * d + tid] - x[s * d + tid];
+    if (tid < d) h[tid] = xn - xc;
+    xc = xn;
+    xn = xnn;
     __syncthreads();
     for (int m = M; m >= 1; --m) {
       float *Sm = lev + off[m];
       for (int e = tid; e < sz[m]; e += nth) {
-        float acc = 0.0f, P = 1.0f, fact = 1.0f;
+        float acc = 0.0f, P = 1.0f;
         int pre = e;
         for (int j = m - 1; j >= 0; --j) {
           const int q = dv.div(pre), digit = pre - q * d;
           pre = q;
           P *= h[digit];
-          fact *= (float)(m - j);
           const float Sj = (j == 0) ? 1.0f : lev[off[j] + pre];
-          acc = __builtin_fmaf(Sj, P / fact, acc);
+          acc = __builtin_fmaf(Sj, P * c_invfact[m - j], acc);
         }
         Sm[e] += acc;
       }
@@ -132,15 +142,14 @@ __global__ __launch_bounds__(256) void sig_features_bwd_kernel(SigFeatArgs a, co
     for (int m = M; m >= 1; --m) {
       float *Sm = lev + off[m];
       for (int e = tid; e < sz[m]; e += nth) {
-        float acc = 0.0f, P = 1.0f, fact = 1.0f;
+        float acc = 0.0f, P = 1.0f;
         int pre = e;
         for (int j = m - 1; j >= 0; --j) {
           const int q = dv.div(pre), digit = pre - q * d;
           pre = q;
           P *= h[digit];
-          fact *= (float)(m - j);
           const float Sj = (j == 0) ? 1.0f : lev[off[j] + pre];
-          acc = __builtin_fmaf(Sj, P / fact, acc);
+          acc = __builtin_fmaf(Sj, P * c_invfact[m - j], acc);
         }
         Sm[e] += acc;
       }
@@ -152,15 +161,14 @@ __global__ __launch_bounds__(256) void sig_features_bwd_kernel(SigFeatArgs a, co
   auto fill_E = [&]() {
     for (int r = 1; r <= M; ++r)
       for (int v = tid; v < sz[r]; v += nth) {
-        float P = 1.0f, fact = 1.0f;
+        float P = 1.0f;
         int w = v;
         for (int p = 0; p < r; ++p) {
           const int q = dv.div(w);
           P *= h[w - q * d];
           w = q;
-          fact *= (float)(p + 1);
         }
-        Et[off[r] + v] = P / fact;
+        Et[off[r] + v] = P * c_invfact[r];
       }
   };
   for (int s = 0; s + 1 < a.l; ++s) {
@@ -169,6 +177,7 @@ __global__ __launch_bounds__(256) void sig_features_bwd_kernel(SigFeatArgs a, co
     __syncthreads();
     chen();
   }
+  float ghp = 0.0f;  // (tid < d) dh of the step after this one
   for (int s = a.l - 2; s >= 0; --s) {
     if (tid < d) {
       h[tid] = -(x[(s + 1) * d + tid] - x[s * d + tid]);
@@ -208,9 +217,7 @@ __global__ __launch_bounds__(256) void sig_features_bwd_kernel(SigFeatArgs a, co
     for (int q = 0; q < GH_REG; ++q) ghr[q] = 0.0f;
     for (int r = 1; r <= M; ++r)
       for (int v = tid; v < sz[r]; v += nth) {
-        const float ge = gE[off[r] + v];
-        float fact = 1.0f;
-        for (int p = 1; p <= r; ++p) fact *= (float)p;
+        const float ge = gE[off[r] + v] * c_invfact[r];
         // digits of v (most significant first is irrelevant: the product is symmetric)
         int vv = v;
         for (int p = 0; p < r; ++p) {
@@ -223,7 +230,7 @@ __global__ __launch_bounds__(256) void sig_features_bwd_kernel(SigFeatArgs a, co
             if (p2 != p) P *= h[w - wq * d];
             w = wq;
           }
-          const float val = ge * P / fact;
+          const float val = ge * P;
           if (d <= GH_REG) {
 #pragma unroll
             for (int q2 = 0; q2 < GH_REG; ++q2) ghr[q2] += (q2 == q) ? val : 0.0f;  // no dynamic register index
@@ -259,11 +266,14 @@ __global__ __launch_bounds__(256) void sig_features_bwd_kernel(SigFeatArgs a, co
       }
       __syncthreads();
     }
+    // dx_{s+1} += dh_s, dx_s -= dh_s: point s+1 takes dh_s - dh_{s+1} now (each point's gradient is read and
+    // written once, so no step waits on the previous step's store to the same address)
     if (tid < d) {
-      gx[(s + 1) * d + tid] += gh[tid];
-      gx[s * d + tid] -= gh[tid];
+      gx[(s + 1) * d + tid] += gh[tid] - ghp;
+      ghp = gh[tid];
     }
   }
+  if (tid < d && a.l > 1) gx[tid] -= ghp;
 }
 
 }  // namespace gpsig
