@@ -29,7 +29,8 @@ bool ho_bwd_supported(int l2, int order, int M, int seed) {
   if (seed != SEED_RBF_DIFF && seed != SEED_LIN_DIFF) return false;
   if (l2 < 2 || M < 2 || M > 8 || order < 2) return false;
   const int o = ho_eff_order(order, M);
-  if (l2 > HO_SPLIT_NW * HO_SPLIT_CPB + 1) return o <= HO_LDS_MAX_ORD && ho_bwd_split8_fits(o, M, l2);
+  if (l2 > HO_SPLIT_NW * HO_SPLIT_CPB + 1 && o <= HO_LDS_MAX_ORD && ho_bwd_split8_fits(o, M, l2)) return true;
+  if (l2 > 512) return false;
   return ho_bwd_reg(l2, o, M) || (o <= HO_LDS_MAX_ORD && ho_bwd_lds_fits(o, M, l2));
 }
 

@@ -80,7 +80,8 @@ static bool split_on() {
 
 template <int ORD, int M>
 static int launch_lds_w(const BwdArgs &a, int seed, long long nblocks, hipStream_t s) {
-  if (a.l2 > HO_SPLIT_NW * HO_SPLIT_CPB + 1) return launch_split8<ORD, M>(a, seed, nblocks, s);
+  // 510 .. 512 points at (order, levels) the 8-wave form does not hold keep the one-wave W = 8 kernel
+  if (a.l2 > HO_SPLIT_NW * HO_SPLIT_CPB + 1 && ho_split8_ok(ORD, M)) return launch_split8<ORD, M>(a, seed, nblocks, s);
   if (a.l2 <= 256) return launch_lds<ORD, M, 4>(a, seed, nblocks, s);
   if (split_on() && ho_bwd_split_fits(ORD, M, a.l2)) return launch_split<ORD, M>(a, seed, nblocks, s);
   return launch_lds<ORD, M, 8>(a, seed, nblocks, s);

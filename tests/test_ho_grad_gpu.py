@@ -105,6 +105,8 @@ def _walks(n, l, d, seed):
     (381, 3, 4, 3, "rbf"), (509, 2, 3, 2, "linear"),
     # effective order 6 (6 levels, up to 256 points: the LDS-state kernel at W = 4)
     (20, 3, 6, 6, "rbf"), (18, 2, 6, 7, "rbf"), (200, 2, 6, 6, "linear"),
+    # 510-512 points at levels the 8-wave form does not hold: the one-wave W = 8 kernel
+    (511, 2, 7, 3, "linear"),
 ])
 def test_higher_order_vjp_kernel_raw_levels(L, D, M, order, base):
     """gpsig_sig_gram_vjp_ho (csrc/sig_ho_bwd.h, sig_ho_bwd_lds.h) against fp64 autodiff of
