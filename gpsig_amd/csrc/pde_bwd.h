@@ -31,6 +31,8 @@
 // Three sweeps of the grid instead of the previous two sweeps plus an fp64 K_rev grid stored and
 // re-read through HBM (~0.3 MB per pair at L = 100, dyadic 1).
 #pragma once
+#include <type_traits>
+
 #include "sig_common.h"
 
 namespace gpsig {
@@ -146,6 +148,9 @@ __device__ __forceinline__ void pde_adj_body(const PdeBwdArgs &p, double *ldsd) 
   constexpr int WC = W / REP;
   constexpr int WC2 = (WC + 1) / 2;  // coarse columns in packed fp32 pairs (the contractions)
   constexpr int H = pde_chunk<W, REP>();
+  // the chunk's K corners: fp64 up to 32 values per lane (the narrow geometries, where 32 more VGPRs keep the
+  // occupancy), fp32 beyond
+  using KC = typename std::conditional<(H * REP * W <= 32 && W <= 4), double, float>::type;
   constexpr int FW = W + REP;  // front words per lane: up[W], last[0 .. REP-2], corner_prev
   constexpr int CB = 64 * W;   // fine columns per block
   const int lane = threadIdx.x & 63;
@@ -251,7 +256,8 @@ __device__ __forceinline__ void pde_adj_body(const PdeBwdArgs &p, double *ldsd) 
     corner_prev = 1.0;
   };
   // inco: the step's coarse increments (pass B's R sweep of the same step reuses them)
-  auto kstep = [&](int s, float (&kc)[REP][W], double (&inco)[WC]) {
+  // kc: KC (fp32 where the registers are short, fp64 otherwise: no conversions per cell)
+  auto kstep = [&](int s, KC (&kc)[REP][W], double (&inco)[WC]) {
     double left[REP];
 #pragma unroll
     for (int r = 0; r < REP; ++r) left[r] = lane_prev(last[r]);
@@ -292,7 +298,7 @@ __device__ __forceinline__ void pde_adj_body(const PdeBwdArgs &p, double *ldsd) 
               kn = (upw + lft) * (1.0 + 0.5 * t + (1.0 / 12) * t2) - cor * (1.0 - (1.0 / 12) * t2);
             }
           }
-          kc[r][w] = (float)cor;
+          kc[r][w] = (KC)cor;
           cor = upw;
           lft = kn;
           up[w] = kn;
@@ -321,7 +327,7 @@ __device__ __forceinline__ void pde_adj_body(const PdeBwdArgs &p, double *ldsd) 
 #pragma unroll
       for (int h = 0; h < H; ++h) {
         // steps past nsteps (the last chunk's tail) touch no cell: ci >= IC in every lane used
-        float kc[REP][W];
+        KC kc[REP][W];
         double incd[WC];
         const int s = s0 + h;
         kstep(s, kc, incd);
@@ -386,7 +392,7 @@ __device__ __forceinline__ void pde_adj_body(const PdeBwdArgs &p, double *ldsd) 
       last[REP - 1] = up[W - 1];
       corner_prev = (double)fv[W + REP - 1];
       if (s0 >= H) ldfront(s0 - H);
-      float kc[H][REP][W];
+      KC kc[H][REP][W];
       double incH[H][WC];
 #pragma unroll
       for (int w2 = 0; w2 < WC2; ++w2)
@@ -426,7 +432,7 @@ __device__ __forceinline__ void pde_adj_body(const PdeBwdArgs &p, double *ldsd) 
               const double rn = (upw + rgt) + cor * inc[w / REP];
               // KK[i][c] = K(i, c) * R(i+1, c+1) = K[i][c] * K_rev[I-1-i][J-1-c] (columns >= J: R = 1,
               // their sums meet dy = 0 and are not stored)
-              S[w / REP] = __builtin_fma((double)kc[h][r][w], cor, S[w / REP]);
+              S[w / REP] = __builtin_fma((double)kc[h][r][w], cor, S[w / REP]);  // (no-op cast for fp64 KC)
               cor = upw;
               rgt = rn;
               ru[w] = rn;
