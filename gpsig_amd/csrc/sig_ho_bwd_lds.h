@@ -125,17 +125,21 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(1))) void si
     if constexpr (RC > 3) one(std::integral_constant<int, 3>{});
   };
 
-  // an empty volatile statement on v: orders the computation of v with the slab accesses around it
-  auto pin = [&](float (&v)[W]) {
-#pragma unroll
-    for (int w = 0; w < W; ++w) asm volatile("" : "+v"(v[w]));
-  };
-  // the multiplier slab: slot s of this lane's W columns
-  float *__restrict__ ps = pslab + lane * W;
   // Compiler barriers around the slab accesses bound the register use where the slab is large (W = 8, or many
   // slots): without them a level's reads are hoisted and the kernel spills (W = 4 at 7 levels).  Small slabs
   // go without: the reads of a level batch ahead of their use (each lane touches only its own columns).
   constexpr bool FENCE = W > 4 || Lay::np + Lay::ncb > HO_LDS_NOFENCE_SLOTS;
+  // an empty volatile statement on v: orders the computation of v with the slab accesses around it (with the
+  // barriers, and for slabs past 60 slots; otherwise the accumulation is scheduled freely)
+  constexpr bool PIN = FENCE || Lay::np + Lay::ncb > 60;  // unpinned past 60 slots the W = 4 kernel spills
+  auto pin = [&](float (&v)[W]) {
+    if constexpr (PIN) {
+#pragma unroll
+      for (int w = 0; w < W; ++w) asm volatile("" : "+v"(v[w]));
+    }
+  };
+  // the multiplier slab: slot s of this lane's W columns
+  float *__restrict__ ps = pslab + lane * W;
   auto pget = [&](int slot, float (&v)[W]) {
     if constexpr (FENCE) asm volatile("" ::: "memory");
 #pragma unroll
