@@ -156,6 +156,24 @@ def _folded(cfg, X2s, lengths, needs_grad):
     return _ho_vjp_kernel(cfg, *lengths)
 
 
+FOLD_WEIGHT_BYTES = int(os.environ.get("GPSIG_FOLD_WEIGHT_BYTES", 1 << 30))
+
+
+def _fold_blocks(n1, n2, M, budget=None):
+    """Row / column block sizes of the folded K(X, X2) backward.  One upper-triangle launch over the whole
+    concatenation [X; X2] evaluates (n1 + n2)^2 / 2 pairs for the n1 n2 of the X-X2 block and its (M+1)
+    (n1 + n2)^2 fp64 weights: fine while the two sides are comparable (at most 2x the pairs) and the weights
+    fit `budget`; otherwise the larger side (or both) is cut into blocks of about the smaller side, at least
+    128 rows, so every launch carries at most ~2x its useful pairs and its weights stay within the budget."""
+    budget = FOLD_WEIGHT_BYTES if budget is None else budget
+    per = 12 * (M + 1)  # fp64 weights + their fp32 copy, per pair slot
+    if max(n1, n2) <= 2 * min(n1, n2) and per * (n1 + n2) ** 2 <= budget:
+        return n1, n2
+    b = max(min(n1, n2), 128)
+    b = max(1, min(b, int((budget / per) ** 0.5) // 2))
+    return min(n1, b), min(n2, b)
+
+
 def _epilogue_cross(Kr, d1, d2, sc, cfg):
     """kernels.py:457-470: K(X, X2) over the square roots of the two raw diagonals + jitter, sigma * variances."""
     K = Kr / (torch.sqrt(d1 + cfg["jitter"])[:, :, None] * torch.sqrt(d2 + cfg["jitter"])[:, None, :])
@@ -259,15 +277,30 @@ class SigGram(torch.autograd.Function):
             n1, l1 = Xs.shape[:2]
             n2, l2 = X2s.shape[:2]
             lm = max(l1, l2)
-            Xc = torch.cat([_pad_last(Xs.detach().to(torch.float32), lm), _pad_last(X2s.detach().to(torch.float32), lm)])
-            Gc = torch.zeros((M + 1, n1 + n2, n1 + n2), dtype=torch.float64, device=Xs.device)
-            Gc[:, :n1, n1:] = gK
-            idx1 = torch.arange(n1, device=Xs.device)
-            idx2 = torch.arange(n1, n1 + n2, device=Xs.device)
-            Gc[:, idx1, idx1] = g1
-            Gc[:, idx2, idx2] = g2
-            gXc, _ = ops.sig_gram_vjp(Xc, None, M, Gc.to(torch.float32), **vjp)
-            gX, gY = _unpad_grad(gXc[:n1], l1), _unpad_grad(gXc[n1:], l2)
+            Xp = _pad_last(Xs.detach().to(torch.float32), lm)
+            X2p = _pad_last(X2s.detach().to(torch.float32), lm)
+            gX = torch.zeros(Xp.shape, dtype=torch.float64, device=Xs.device)
+            gY = torch.zeros(X2p.shape, dtype=torch.float64, device=Xs.device)
+            b1, b2 = _fold_blocks(n1, n2, M)
+            # one launch per block pair (rows r of X, rows c of X2) over [X_r; X2_c]: the X-X2 weights of the
+            # block, X_r's diagonal terms in the first column block, X2_c's in the first row block
+            for r0 in range(0, n1, b1):
+                r1 = min(n1, r0 + b1)
+                for c0 in range(0, n2, b2):
+                    c1 = min(n2, c0 + b2)
+                    m1, m2 = r1 - r0, c1 - c0
+                    Gc = torch.zeros((M + 1, m1 + m2, m1 + m2), dtype=torch.float64, device=Xs.device)
+                    Gc[:, :m1, m1:] = gK[:, r0:r1, c0:c1]
+                    if c0 == 0:
+                        i1 = torch.arange(m1, device=Xs.device)
+                        Gc[:, i1, i1] = g1[:, r0:r1]
+                    if r0 == 0:
+                        i2 = torch.arange(m1, m1 + m2, device=Xs.device)
+                        Gc[:, i2, i2] = g2[:, c0:c1]
+                    gXc, _ = ops.sig_gram_vjp(torch.cat([Xp[r0:r1], X2p[c0:c1]]), None, M, Gc.to(torch.float32), **vjp)
+                    gX[r0:r1] += gXc[:m1]
+                    gY[c0:c1] += gXc[m1:]
+            gX, gY = _unpad_grad(gX, l1), _unpad_grad(gY, l2)
             return (gX.to(Xs.dtype) if ctx.needs_input_grad[0] else None,
                     gY.to(X2s.dtype) if ctx.needs_input_grad[1] else None,
                     gsc.to(ctx.scale_dtype) if ctx.needs_input_grad[2] else None, None)

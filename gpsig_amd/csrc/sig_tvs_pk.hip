@@ -173,7 +173,8 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(INCR ? GPSIG
           // arguments past the polynomial range: expm1 = e^x - 1 (no cancellation there)
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
-            if (!(__builtin_fabsf(qv[h]) < EM1_TAU)) Eq[h] = __builtin_amdgcn_exp2f(qv[h] * L2E) - 1.0f;
+            // (finite: e^q past FLT_MAX only multiplies an underflowed carry, where 0 * inf would be NaN)
+            if (!(__builtin_fabsf(qv[h]) < EM1_TAU)) Eq[h] = __builtin_fminf(__builtin_amdgcn_exp2f(qv[h] * L2E) - 1.0f, 3.0e38f);
             if constexpr (INCR)
               if (!(__builtin_fabsf(cv[h]) < EM1_TAU)) Ec[h] = __builtin_amdgcn_exp2f(cv[h] * L2E) - 1.0f;
           }

@@ -96,11 +96,13 @@ def test_gram_vjp_shapes(D, M, L):
     k = gpsig_amd.SignatureRBF(L * D, D, M)
     got, _ = grads_gpu(k, X, None, G)
     ref, _, _, _ = grads_ref(X, None, G, M)
+    assert norm_rel_err(got[0], ref[0]) < (2e-5 if (D, M, L) == (1, 1, 8) else GTOL)
     # (D, M, L) = (1, 1, 8): one channel, level 1 only, normalised -- the gradient is a difference of corner
-    # terms that cancel across pairs; measured 1.0e-5 (fp32 autodiff of the reference graph: 4.0e-3; fp64 at the
-    # fp32-rounded inputs: 6.2e-8), named in DESIGN.md 2.6 with its own bound
-    tol = 2e-5 if (D, M, L) == (1, 1, 8) else GTOL
-    assert norm_rel_err(got[0], ref[0]) < tol
+    # terms that cancel across pairs, so the fp32 rounding of the inputs the kernel receives moves it by
+    # ~1e-5 of its size (fp32 autodiff of the reference graph: 4.0e-3).  Every shape is also held to the plain
+    # GTOL against fp64 autodiff of the reference graph at those fp32-rounded inputs (what the GPU computes on).
+    ref_q, _, _, _ = grads_ref(X.astype(np.float32).astype(np.float64), None, G, M)
+    assert norm_rel_err(got[0], ref_q[0]) < GTOL
 
 
 @pytest.mark.parametrize("base", ["rbf", "linear"])

@@ -48,14 +48,36 @@ def test_higher_order_signature_kernel_gradient(normalization, cross, return_lev
     assert norm_rel_err(Xt.grad.reshape(X.shape).cpu().numpy(), Xr.grad.numpy()) < GTOL
     if cross:
         assert norm_rel_err(X2t.grad.reshape(X2.shape).cpu().numpy(), X2r.grad.numpy()) < GTOL
-    # dLoss/dl_k = -sum_i x_ik dLoss/dx_ik / l_k is a contraction over every point: on these inputs its terms
-    # cancel up to ~2000x ("lengthscale gradients"), so it is held to GTOL times the sum of
-    # the terms' magnitudes, the forward-error bound of that sum -- measured 2.5e-5..3.4e-5 max-relative
+    # dLoss/dl_k = -sum_i x_ik dLoss/dx_ik / l_k is a contraction over every point whose terms cancel up to
+    # ~2000x on these inputs, so the fp32 rounding of the scaled inputs the kernels receive
+    # (x / l -> fp32, ~6e-8 relative) moves the exact lengthscale gradient by ~1e-5 of its size.  The
+    # criterion is therefore the plain 1e-5 against fp64 autodiff of the reference graph evaluated at those
+    # fp32-rounded scaled inputs (what the GPU computes on), with the lengthscale chain rule applied in fp64.
+    Xq = _fp32_scaled(X, ls)
+    X2q = None if X2 is None else _fp32_scaled(X2, ls)
+    xs = torch.tensor(Xq, requires_grad=True)
+    x2s = None if X2q is None else torch.tensor(X2q, requires_grad=True)
+    vq = torch.tensor(var, requires_grad=True)
+    Kq = ar.K(xs, x2s, M, base="linear", normalization=normalization, scale=vq, return_levels=return_levels, order=M)
+    (Kq * torch.tensor(G)).sum().backward()
+    gl_q = -(X * xs.grad.numpy()).reshape(-1, D).sum(0) / ls ** 2
+    if cross:
+        gl_q = gl_q - (X2 * x2s.grad.numpy()).reshape(-1, D).sum(0) / ls ** 2
+    assert norm_rel_err(k.lengthscales.grad.cpu().numpy(), gl_q) < GTOL
+    assert norm_rel_err(Xt.grad.reshape(X.shape).cpu().numpy(), xs.grad.numpy() / ls) < GTOL
+    assert norm_rel_err(k.variances.grad.cpu().numpy(), vr.grad.numpy()) < GTOL
+    # and against the exact inputs, held to the forward-error bound of the cancelling sum (GTOL times the sum
+    # of the terms' magnitudes): the size of the input-rounding effect above
     terms = np.abs(X * Xr.grad.numpy()).reshape(-1, D).sum(0)
     if cross:
         terms = terms + np.abs(X2 * X2r.grad.numpy()).reshape(-1, D).sum(0)
     assert (np.abs(k.lengthscales.grad.cpu().numpy() - lr.grad.numpy()) <= GTOL * terms / ls).all()
-    assert norm_rel_err(k.variances.grad.cpu().numpy(), vr.grad.numpy()) < GTOL
+
+
+def _fp32_scaled(X, ls):
+    """The scaled sequences as the kernels receive them: x / l in float64 (kernels.py:344-365, the host
+    scaling) rounded to float32 (ops._f32), back in float64 for the fp64 reference."""
+    return (X / ls).astype(np.float32).astype(np.float64)
 
 
 def test_higher_order_diag_and_norms_gradient():
@@ -332,3 +354,26 @@ def test_higher_order_vjp_past_512_points(L, D, M, order, base):
     Xr = torch.tensor(X, requires_grad=True)
     (ar.k_seq_diag(Xr, M, base, order=order) * torch.tensor(Gd)).sum().backward()
     assert norm_rel_err(gD.cpu().numpy(), Xr.grad.numpy()) < GTOL
+
+
+def test_folded_cross_backward_in_blocks(monkeypatch):
+    """The folded K(X, X2) backward cut into block launches (autograd._fold_blocks: lopsided shapes or
+    weights past GPSIG_FOLD_WEIGHT_BYTES) gives the gradient of the single launch, against fp64 autodiff."""
+    import gpsig_amd
+    from gpsig_amd import autograd as ag
+    g = golden("linear_chen.npz")
+    X = g["X"]
+    N, L, D = X.shape
+    M = int(g["num_levels"])
+    X2 = np.cumsum(np.random.default_rng(3).standard_normal((7, L, D)), 1) / np.sqrt(L * D)
+    G = np.random.default_rng(4).standard_normal((N, 7))
+    monkeypatch.setattr(ag, "_fold_blocks", lambda n1, n2, M, budget=None: (5, 3))
+    k = gpsig_amd.SignatureLinear(L * D, D, M, order=M)
+    Xt = torch.tensor(X.reshape(N, -1), device=DEV, requires_grad=True)
+    X2t = torch.tensor(X2.reshape(7, -1), device=DEV, requires_grad=True)
+    (k.K(Xt, X2t) * torch.as_tensor(G, device=DEV)).sum().backward()
+    Xr = torch.tensor(X, requires_grad=True)
+    X2r = torch.tensor(X2, requires_grad=True)
+    (ar.K(Xr, X2r, M, base="linear", order=M) * torch.tensor(G)).sum().backward()
+    assert norm_rel_err(Xt.grad.reshape(X.shape).cpu().numpy(), Xr.grad.numpy()) < GTOL
+    assert norm_rel_err(X2t.grad.reshape(X2.shape).cpu().numpy(), X2r.grad.numpy()) < GTOL
