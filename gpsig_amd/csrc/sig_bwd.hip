@@ -1,7 +1,7 @@
 // gpsig_amd -- extern "C" entry of the first-order Gram VJP (include/gpsig_amd.h, gpsig_sig_gram_vjp):
 // argument checks, feature records, tile counts, dispatch to the per-(DP, M) instantiations of
 // sig_bwd_kernel (sig_bwd.h, sig_bwd_inst.hip).
-#include "sig_bwd.h"
+#include "sig_bwd_pk.h"
 
 namespace gpsig {
 int features(const float *X, int n, int l, int d, int DP, float *F, hipStream_t s);
@@ -24,6 +24,42 @@ static int vjp_fixed_max() {
 static bool bwd_wide(int d) { return d > vjp_fixed_max(); }
 template <int DP, int M>
 int sig_bwd_launch_dpm(const BwdArgs &a, int seed, long long nblocks, hipStream_t s);
+template <int DP, int M>
+int sig_bwd_pk_launch_dpm(const BwdArgs &a, int seed, BwdGeo geo, long long nblocks, hipStream_t s);
+
+// The packed column-pair VJP (sig_bwd_pk.h) for the difference seeds in one column block; GPSIG_BWD_PK=0
+// keeps sig_bwd_kernel everywhere (A/B runs)
+static bool bwd_pk_enabled() {
+  static const bool v = [] {
+    const char *e = getenv("GPSIG_BWD_PK");
+    return !(e && atoi(e) == 0);
+  }();
+  return v;
+}
+// Measured (tools/kbench_vjp.hip, N = 1024, D = 5, M = 5, saved state; profiles/r6_vjp_ab.txt): at the same
+// geometry the packed kernel is 1-4 % faster (L = 64: 11.12 -> 10.99 ms, L = 128: 27.28 -> 26.13 ms), but at
+// 65-100 points sig_bwd_kernel's 20-lane groups (3 pairs per wave, W = 5) beat its 32-lane W = 4 (2 pairs):
+// C2 21.79 vs 24.15 ms.  So the packed kernel takes every one-block shape except that segmented geometry.
+static BwdGeo bwd_pk_geo(int l2, int DP, int M, int seed) {
+  if (!bwd_pk_enabled() || (seed != SEED_RBF_DIFF && seed != SEED_LIN_DIFF)) return {0, 0};
+  const BwdGeo old = bwd_geometry(l2, DP, M);
+  if (old.LP == 20) return {0, 0};
+  return bwd_pk_geometry(l2, DP, M, seed == SEED_RBF_DIFF);
+}
+template <int DP>
+static int bwd_pk_dp(const BwdArgs &a, int seed, BwdGeo geo, long long nblocks, hipStream_t s) {
+  switch (a.M) {
+    case 1: return sig_bwd_pk_launch_dpm<DP, 1>(a, seed, geo, nblocks, s);
+    case 2: return sig_bwd_pk_launch_dpm<DP, 2>(a, seed, geo, nblocks, s);
+    case 3: return sig_bwd_pk_launch_dpm<DP, 3>(a, seed, geo, nblocks, s);
+    case 4: return sig_bwd_pk_launch_dpm<DP, 4>(a, seed, geo, nblocks, s);
+    case 5: return sig_bwd_pk_launch_dpm<DP, 5>(a, seed, geo, nblocks, s);
+    case 6: return sig_bwd_pk_launch_dpm<DP, 6>(a, seed, geo, nblocks, s);
+    case 7: return sig_bwd_pk_launch_dpm<DP, 7>(a, seed, geo, nblocks, s);
+    case 8: return sig_bwd_pk_launch_dpm<DP, 8>(a, seed, geo, nblocks, s);
+    default: return GPSIG_EUNSUPPORTED;
+  }
+}
 
 template <int DP>
 static int bwd_dp(const BwdArgs &a, int seed, long long nblocks, hipStream_t s) {
@@ -135,10 +171,12 @@ extern "C" int gpsig_sig_gram_vjp(const float *X, int n1, int l1, const float *Y
   if (wide)
     return tile_vjp(X, n1, l1, Y, n2, l2, d, num_levels, 1, seed, pair_mode, row_begin, row_end, gout, gout_levels,
                     rs1, rs2, scale, jitter, gX, gY, grs1, grs2, gscale, state, workspace, workspace_bytes, s);
-  const BwdGeo geo = bwd_geometry(l2, DP, num_levels);
+  const BwdGeo pkgeo = bwd_pk_geo(l2, DP, num_levels, seed);
+  const bool pk = pkgeo.W != 0;
+  const BwdGeo geo = pk ? pkgeo : bwd_geometry(l2, DP, num_levels);
   if (geo.W == 0) return GPSIG_EUNSUPPORTED;
   if (row_end == row_begin) return GPSIG_OK;
-  const int nblk = bwd_blocks(l2, difference != 0, geo);
+  const int nblk = pk ? 1 : bwd_blocks(l2, difference != 0, geo);
   const long long scr_stride = bwd_scratch_floats(difference ? l1 - 1 : l1, num_levels, geo.W, nblk);
 
   const bool same = (X == Y && n1 == n2 && l1 == l2);
@@ -206,7 +244,7 @@ extern "C" int gpsig_sig_gram_vjp(const float *X, int n1, int l1, const float *Y
     const long long nb = nblocks - c < chunk ? nblocks - c : chunk;
     switch (DP) {
 #define CASE(v) \
-  case v: rc = bwd_dp<v>(a, seed, nb, s); break;
+  case v: rc = pk ? bwd_pk_dp<v>(a, seed, geo, nb, s) : bwd_dp<v>(a, seed, nb, s); break;
       CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(8) CASE(16)
 #undef CASE
       default: return GPSIG_EUNSUPPORTED;

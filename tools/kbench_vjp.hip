@@ -6,7 +6,7 @@
 #include <cstdlib>
 #include <vector>
 
-#include "../gpsig_amd/csrc/sig_bwd.h"
+#include "../gpsig_amd/csrc/sig_bwd_pk.h"
 
 #ifndef VARIANT
 #define VARIANT "default"
@@ -25,6 +25,12 @@
 #endif
 #ifndef KLP
 #define KLP 32
+#endif
+#ifndef KPK  // 1: the packed column-pair kernel (sig_bwd_pk.h)
+#define KPK 0
+#endif
+#ifndef KSTATE  // 1: a (zero) saved forward state, as the training step's VJP launch
+#define KSTATE 0
 #endif
 
 using namespace gpsig;
@@ -94,6 +100,13 @@ int main(int argc, char **argv) {
   p.g_lvl = (long long)n * n;
   p.gX = p.gY = dGX;
   p.nblk = 1;
+  if (KSTATE) {
+    float *dS;
+    const size_t sb = (size_t)n * (n + 1) / 2 * state_stride(M, l) * 4;
+    CK(hipMalloc(&dS, sb));
+    CK(hipMemset(dS, 0, sb));
+    p.state = dS;
+  }
   const int G_ = 64 / KLP;
   const long long ntb = (n + G_ - 1) / G_, nta = (n + 3) / 4;
   p.ntb = (int)ntb;
@@ -102,7 +115,10 @@ int main(int argc, char **argv) {
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
   auto launch = [&]() {
-    hipLaunchKernelGGL((sig_bwd_kernel<DP, KW, KLP, KM, SEED_RBF_DIFF>), dim3((unsigned)nblocks), dim3(256), 0, 0, p);
+    if constexpr (KPK)
+      hipLaunchKernelGGL((sig_bwd_pk_kernel<DP, KW, KLP, KM, SEED_RBF_DIFF>), dim3((unsigned)nblocks), dim3(256), 0, 0, p);
+    else
+      hipLaunchKernelGGL((sig_bwd_kernel<DP, KW, KLP, KM, SEED_RBF_DIFF>), dim3((unsigned)nblocks), dim3(256), 0, 0, p);
   };
   CK(hipMemset(dGX, 0, (size_t)n * l * d * 4));
   launch();
@@ -117,6 +133,7 @@ int main(int argc, char **argv) {
   CK(hipEventSynchronize(e1));
   float ms;
   CK(hipEventElapsedTime(&ms, e0, e1));
-  printf("%s n=%d L=%d D=%d M=%d W=%d LP=%d ms=%.3f chk=%.9e\n", VARIANT, n, l, d, M, KW, KLP, ms / reps, cs);
+  printf("%s n=%d L=%d D=%d M=%d W=%d LP=%d pk=%d state=%d ms=%.3f chk=%.9e\n", VARIANT, n, l, d, M, KW, KLP, KPK, KSTATE,
+         ms / reps, cs);
   return 0;
 }
