@@ -85,6 +85,105 @@ def _ho_vjp_kernel(cfg, *lengths):
             and all(ops.ho_vjp_supported(l, cfg["num_levels"], cfg["order"], cfg["base"]) for l in lengths))
 
 
+def _word_counts(d, m, device):
+    """(d^m, d) float64: occurrences of each channel in each word of length m (iisignature's first-index-major
+    order: word index = w_1 d^(m-1) + ... + w_m)."""
+    idx = torch.arange(d ** m, device=device)
+    cnt = torch.zeros((d ** m, d), dtype=torch.float64, device=device)
+    for k in range(m):
+        digit = (idx // d ** (m - 1 - k)) % d
+        cnt[idx, digit] += 1.0
+    return cnt
+
+
+SCALING_FEATURE_BYTES = int(os.environ.get("GPSIG_SCALING_FEATURE_BYTES", 1 << 28))
+
+
+def _scaling_closed_form(cfg, Xs, X2s=None):
+    """The exact signature kernel, and its fp64 signature features within SCALING_FEATURE_BYTES (beyond it the
+    VJP's own gradient stands: d^M features per sequence make the closed form cost more than it saves)."""
+    if not _ho_signature_case(cfg):
+        return False
+    d, M = Xs.shape[-1], cfg["num_levels"]
+    n = Xs.shape[0] + (0 if X2s is None else X2s.shape[0])
+    return 8 * n * sum(d ** m for m in range(1, M + 1)) <= SCALING_FEATURE_BYTES
+
+
+def _signature64(X, M):
+    """fp64 truncated signatures (n, sum_m d^m) of X (n, l, d), levels 1..M first-index-major: each step's
+    tensor exponential, then Chen's identity S(a * b)_m = sum_k S(a)_k (x) S(b)_(m-k) over a pairwise tree
+    (log2 l rounds), rows in chunks within SCALING_FEATURE_BYTES.  (The fp32 signature kernel's ~3e-7 relative
+    error would be amplified by the cancellation the contraction below exists to avoid.)"""
+    n, l, d = X.shape
+    ch = sum(d ** m for m in range(1, M + 1))
+    out = torch.zeros((n, ch), dtype=torch.float64, device=X.device)
+    if l < 2 or n == 0:
+        return out
+    rows = max(1, SCALING_FEATURE_BYTES // (3 * 8 * (l - 1) * ch))
+    for r0 in range(0, n, rows):
+        dx = (X[r0:r0 + rows, 1:] - X[r0:r0 + rows, :-1]).double()
+        E = [None, dx]
+        for m in range(2, M + 1):
+            E.append((E[-1][..., :, None] * dx[..., None, :]).flatten(-2) / m)
+        while E[1].shape[1] > 1:
+            if E[1].shape[1] % 2:  # a zero step: its exponential is the identity
+                E = [None] + [torch.cat([e, torch.zeros_like(e[:, :1])], 1) for e in E[1:]]
+            A = [None] + [e[:, 0::2] for e in E[1:]]
+            B = [None] + [e[:, 1::2] for e in E[1:]]
+            E = [None] + [A[m] + B[m] + sum((A[k][..., :, None] * B[m - k][..., None, :]).flatten(-2)
+                                            for k in range(1, m)) for m in range(1, M + 1)]
+        out[r0:r0 + rows] = torch.cat([e[:, 0] for e in E[1:]], -1)
+    return out
+
+
+def _scaling_contraction(Xs, X2s, M, gK, gd1=None, gd2=None):
+    """e_c = sum_i x_ic dL/dx_ic (+ the same over X2) for the exact signature kernel (linear, order >= M), in
+    closed form.  Scaling channel c of every sequence by s multiplies each level-m signature coordinate S_w by
+    s^n_c(w) (n_c(w): occurrences of c in the word w), so with K_m(a, b) = <S_m(x_a), S_m(y_b)>,
+        e_c = sum_m 2 sum_w n_c(w) [ sum_ab gK_m(a, b) S_w(x_a) S_w(y_b) + sum_a gd1_m(a) S_w(x_a)^2
+                                      + sum_b gd2_m(b) S_w(y_b)^2 ]
+    from fp64 signatures (_signature64) and one fp64 GEMM per level.  gK (M+1, n1, n2) = dL/d(raw levels)
+    (for K(X) over both slots of every pair), gd1 / gd2 (M+1, n) = dL/d(raw diagonals)."""
+    d = Xs.shape[-1]
+    S1 = _signature64(Xs.detach(), M)
+    S2 = S1 if X2s is None else _signature64(X2s.detach(), M)
+    e = torch.zeros(d, dtype=torch.float64, device=Xs.device)
+    off = 0
+    for m in range(1, M + 1):
+        w = d ** m
+        P, Q = S1[:, off:off + w], S2[:, off:off + w]
+        v = (P * (gK[m].double() @ Q)).sum(0)
+        if gd1 is not None:
+            v = v + (gd1[m].double()[:, None] * P * P).sum(0)
+        if gd2 is not None:
+            v = v + (gd2[m].double()[:, None] * Q * Q).sum(0)
+        e += 2.0 * (v @ _word_counts(d, m, Xs.device))
+        off += w
+    return e
+
+
+def _project_scaling(e, Xs, gX, X2s=None, gY=None):
+    """Adjust the gradient(s) along each channel's scaling direction x_c -> (1 + t) x_c so that their
+    contraction sum_i x_ic g_ic equals e_c (_scaling_contraction), leaving every orthogonal component as the
+    kernels computed it.  That contraction is what the lengthscale gradient reads (dL/dl_c = -e_c / l_c); over
+    the points it cancels (for the normalised kernel sum_c e_c = 0 exactly), so the fp32 VJP's ~1e-6 errors
+    along it would read as ~1e-5 of the lengthscale gradient.  Returns float64 gradients."""
+    X = Xs.detach().double()
+    gX = gX.double()
+    cur = (X * gX).sum(dim=(0, 1))
+    nrm = (X * X).sum(dim=(0, 1))
+    if gY is not None:
+        Y = X2s.detach().double()
+        gY = gY.double()
+        cur = cur + (Y * gY).sum(dim=(0, 1))
+        nrm = nrm + (Y * Y).sum(dim=(0, 1))
+    t = torch.where(nrm > 0, (e - cur) / torch.clamp(nrm, min=1e-300), torch.zeros_like(nrm))
+    gX = gX + X * t
+    if gY is not None:
+        gY = gY + Y * t
+    return gX, gY
+
+
 def _check_bwd(cfg, gram=False):
     """The VJP kernels cover order 1 (difference True or False); Gram / diagonal gradients of higher
     orders are covered by the higher-order VJP kernel (checked by the caller) or, beyond it, for the
@@ -263,6 +362,8 @@ class SigGram(torch.autograd.Function):
                     gK, gsc = torch.autograd.grad(_epilogue(K64, sc, cfg), [K64, sc], gout.double())
                 gX, _ = ops.sig_gram_vjp(Xs.detach(), None, M, gK.to(torch.float32), state=ctx.state, **vjp)
                 ctx.state = None
+                if _scaling_closed_form(cfg, Xs):  # the scaling directions in closed form (lengthscale gradients)
+                    gX, _ = _project_scaling(_scaling_contraction(Xs, None, M, gK), Xs, gX)
                 return (gX.to(Xs.dtype) if ctx.needs_input_grad[0] else None, None,
                         gsc.to(ctx.scale_dtype) if ctx.needs_input_grad[2] else None, None)
             # K(X, X2): the Gram pairs and both sets of diagonal pairs in ONE upper-triangle launch over the
@@ -301,6 +402,8 @@ class SigGram(torch.autograd.Function):
                     gX[r0:r1] += gXc[:m1]
                     gY[c0:c1] += gXc[m1:]
             gX, gY = _unpad_grad(gX, l1), _unpad_grad(gY, l2)
+            if _scaling_closed_form(cfg, Xs, X2s):
+                gX, gY = _project_scaling(_scaling_contraction(Xs, X2s, M, gK, g1, g2), Xs, gX, X2s, gY)
             return (gX.to(Xs.dtype) if ctx.needs_input_grad[0] else None,
                     gY.to(X2s.dtype) if ctx.needs_input_grad[1] else None,
                     gsc.to(ctx.scale_dtype) if ctx.needs_input_grad[2] else None, None)
@@ -333,6 +436,11 @@ class SigGram(torch.autograd.Function):
             if not sym:
                 ops.sig_gram_vjp(X2s.detach(), None, M, grs2 * (-0.5) * rs2 ** 3, base=cfg["base"], diag=True,
                                  difference=cfg["difference"], order=order, gX=gY)
+        if _scaling_closed_form(cfg, Xs, X2s) and not cfg["normalization"]:
+            # unnormalised: dL/dK_m(raw) = gout (per level, or summed) times sigma * variances_m
+            g = gout.double() if cfg["return_levels"] else gout.double()[None].expand(M + 1, -1, -1)
+            gK = g * sc32.double()[:, None, None]
+            gX, gY = _project_scaling(_scaling_contraction(Xs, X2s, M, gK), Xs, gX, X2s, None if sym else gY)
         gXo = gX.to(Xs.dtype) if ctx.needs_input_grad[0] else None
         gYo = gY.to(X2s.dtype) if (not sym and ctx.needs_input_grad[1]) else None
         gso = gscale.to(ctx.scale_dtype) if ctx.needs_input_grad[2] else None
