@@ -34,17 +34,22 @@ constexpr int MF_G = 4;                     // lane groups (x-sequences) per wav
 constexpr int MF_LP = 16;                   // lanes per pair (one DPP row)
 constexpr size_t MF_LDS_MAX = 160 * 1024;
 
-// K padding: KP = 4 KQ with KQ even (every lane's A pair 8-byte aligned): the MFMA loop runs KQ steps per K
-// quarter.  In the LDS B image the four quarters of a column sit QS apart, QS = KQ rounded up to 2 (mod 4), so
-// they are two banks apart (conflict-free ds_read_b64) without padding K itself (round 5: d = 46 ran KQ = 14,
-// 17 % more MFMA work than its KQ = 12; the bank stagger is now in the image's layout, not in K).
+// fp32 record rows are padded to KP = 4 KQ (KQ = ceil(d / 4) rounded up to even) channels.
 __host__ __device__ inline int mf_kq(int d) {
   const int q = (d + 3) / 4;
   return q + (q & 1);
 }
 __host__ __device__ inline int mf_kp(int d) { return 4 * mf_kq(d); }
-__host__ __device__ inline int mf_qs(int kq) { return kq + ((2 - kq % 4) + 4) % 4; }
-__host__ __device__ inline int mf_ldb(int d) { return 4 * mf_qs(mf_kq(d)) + 4; }
+// The GEMM runs on v_mfma_f32_16x16x32_f16 with every fp32 operand split into two halves, a = 2^-e (hi + lo)
+// (hi = f16(2^e a), lo = f16(2^e a - hi), 2^e per sequence putting its largest |value| in [2^13, 2^14)):
+// hi hi' + hi lo' + lo hi' carries 22 of the 24 mantissa bits (products exact in the fp32 accumulator), the
+// same error as the fp32 dot it replaces (|err| / sum |terms| 2.3e-7 vs 2.0e-7 on random walks, d = 46), at a
+// sixteenth of the f32 MFMA's cycles per product (16 cycles per 16x16x32 against 32 per 16x16x4): 3 passes,
+// 5.3x fewer matrix-core cycles.  K is padded to KH = 32 multiples.
+__host__ __device__ inline int mf_kh(int d) { return (d + 31) & ~31; }
+// B image in LDS: column j at j LDBH halves, [hi: KH][lo: KH] + 8 halves of padding (a column stride of
+// 68 mod 64 dwords: the 16 columns of a ds_read_b128 start on distinct 4-bank groups)
+__host__ __device__ inline int mf_ldbh(int d) { return 2 * mf_kh(d) + 8; }
 // columns per lane by sequence length: one tile of LP W columns up to 160 points, past that W = 8 in column
 // blocks of LPW - 1 = 127 cells (the block's last column is the point of its first cell, below)
 __host__ __device__ inline int mf_w(int l) { return l <= 64 ? 4 : (l <= 128 ? 8 : (l <= 160 ? 10 : 8)); }
@@ -56,15 +61,18 @@ __host__ __device__ inline int mf_rows(int l) {
   const int r = (l + 3) & ~3, w = mf_lpw(l);
   return r > w ? r : w;
 }
-// record of a sequence: [aug: rows x KP][points: rows x KP][hd: rows][gg: rows]
+// record of a sequence (floats): [aug: rows x KP][points: rows x KP][hd: rows][gg: rows][2^-e, 2^e, 0, 0]
+// [aug hi: rows x KH halves][aug lo: rows x KH halves]
 //   aug row 0 = x_0, aug row t = x_t - x_{t-1} (1 <= t < l), points row t = x_t; zero past l and past d
+//   (every section 16-byte aligned: rows is a multiple of 4, KP of 8, KH of 32)
+__host__ __device__ inline long long mf_scale_off(int d, int l) { return 2LL * mf_rows(l) * mf_kp(d) + 2LL * mf_rows(l); }
+__host__ __device__ inline long long mf_half_off(int d, int l) { return mf_scale_off(d, l) + 4; }
 __host__ __device__ inline long long mf_rec_floats(int d, int l) {
-  const long long r = mf_rows(l);
-  return 2 * r * mf_kp(d) + 2 * r;
+  return mf_half_off(d, l) + (long long)mf_rows(l) * mf_kh(d);
 }
 inline size_t mf_lds_bytes(int d, int l2, int nw) {
   const size_t lpw = (size_t)mf_lpw(l2);
-  return (lpw * (size_t)mf_ldb(d) + (size_t)nw * 16 * (lpw + 4)) * sizeof(float);
+  return lpw * (size_t)mf_ldbh(d) * 2 + (size_t)nw * 16 * (lpw + 4) * sizeof(float);
 }
 // waves per workgroup: 8 (two per SIMD, so one wave's matrix-core phase overlaps another's recursion) when
 // the LDS allows, else 4 (wide B images: d > 114 at 129..160 points); 0: no tile geometry
@@ -96,8 +104,17 @@ constexpr int MF_BLK_CHUNK = 256;
 inline int mf_cw(int M) { return M <= 5 ? 4 : 8; }
 inline size_t mf_carry_bytes(int l1, int nw) { return (size_t)MF_BLK_CHUNK * nw * MF_G * (size_t)(l1 > 1 ? l1 - 1 : 1) * 8 * sizeof(float); }
 
-// v_mfma_f32_16x16x4_f32: lane l supplies A[l & 15][l >> 4] and B[l >> 4][l & 15]; D row 4 (l >> 4) + r, col l & 15
-GPSIG_DEV f4 mfma16(float a, float b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, c, 0, 0, 0); }
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+// v_mfma_f32_16x16x32_f16: lane l supplies A[l & 15][8 (l >> 4) + e] and B[8 (l >> 4) + e][l & 15], e < 8;
+// D row 4 (l >> 4) + r, col l & 15
+GPSIG_DEV f4 mfma16h(h8 a, h8 b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0); }
+// v = 2^-e (hi + lo) at the sequence's scale 2^e
+GPSIG_DEV h2 mf_split(float v, float sc) {
+  const float b = v * sc;
+  const _Float16 hi = (_Float16)b;
+  return (h2){hi, (_Float16)(b - (float)hi)};
+}
 
 // Wavefront-scope ordering of the wave's own LDS tile between its lanes (writes by one lane, reads by another)
 GPSIG_DEV void wave_lds_sync() {
@@ -120,11 +137,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4)
   constexpr int CPB = LPW - 1;   // cells per column block
   const SigArgs &p = q.p;
   extern __shared__ __attribute__((aligned(16))) float mf_lds[];
-  const int KP = q.kp, KQ = KP / 4, QS = mf_qs(KQ), LDB = 4 * QS + 4;
-  float *__restrict__ Bs = mf_lds;
+  const int KP = q.kp, KH = mf_kh(q.d), LDBH = 2 * KH + 8;
+  _Float16 *__restrict__ Bs = reinterpret_cast<_Float16 *>(mf_lds);
   const int lane = (int)threadIdx.x & 63;
   const int wave = wave_uniform((int)threadIdx.x >> 6);
-  float *__restrict__ Cs = mf_lds + LPW * LDB + wave * 16 * LDC;
+  float *__restrict__ Cs = mf_lds + LPW * LDBH / 2 + wave * 16 * LDC;
   const int g = lane >> 4, gl = lane & 15;
 
   // ---- tile: x-block tx (XB sequences) against y-sequence b
@@ -145,14 +162,18 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4)
   }
   const float *__restrict__ fyb = p.FY + (long long)b * q.ry;
   const float *__restrict__ pty = fyb + (long long)q.rowsy * KP;  // y's points
+  const float sy = fyb[mf_scale_off(q.d, p.l2) + 1], rsy = fyb[mf_scale_off(q.d, p.l2)];  // 2^e_b, 2^-e_b
   // B image of column block j0: column jj < LPW - 1 = aug row j0 + jj + 1 (dy_{j0+jj}), column LPW - 1 = the
-  // point y_{j0}; column stride LDB, K quarter kq of a column at kq QS (k = kq KQ + r at kq QS + r)
+  // point y_{j0}, split into halves at y's scale: column j at j LDBH, hi at k, lo at KH + k
   auto load_b = [&](int j0) {
-    const int k2n = KP / 2;
+    const int k2n = KH / 2;
     for (int e = (int)threadIdx.x; e < LPW * k2n; e += 64 * NW) {
-      const int j = e / k2n, k = 2 * (e - j * k2n), kq = k / KQ;
+      const int j = e / k2n, k = 2 * (e - j * k2n);
       const float *src = j + 1 == LPW ? pty + (long long)j0 * KP : fyb + (long long)(j0 + j + 1) * KP;
-      *reinterpret_cast<f2 *>(Bs + j * LDB + kq * QS + (k - kq * KQ)) = *reinterpret_cast<const f2 *>(src + k);
+      const f2 v = k < KP ? *reinterpret_cast<const f2 *>(src + k) : (f2){0.0f, 0.0f};
+      const h2 s0 = mf_split(v[0], sy), s1 = mf_split(v[1], sy);
+      *reinterpret_cast<h2 *>(Bs + j * LDBH + k) = (h2){s0[0], s1[0]};
+      *reinterpret_cast<h2 *>(Bs + j * LDBH + KH + k) = (h2){s0[1], s1[1]};
     }
   };
   load_b(0);
@@ -175,14 +196,23 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4)
   const bool carries = BLK && M > 1 && nblk > 1;
 
   // ---- GEMM of one chunk (x-rows 4 ch .. 4 ch + 3 of the wave's four sequences) into the wave's tile
-  // A operand of lane l: GEMM row m = l & 15 = 4 (x-sequence) + (chunk row), K quarter l >> 4
-  const float *__restrict__ Asrc;
+  // A operand of lane l: GEMM row m = l & 15 = 4 (x-sequence) + (chunk row), halves 8 (l >> 4) .. + 7 of
+  // every 32-channel step, from the x record's hi / lo rows
+  const _Float16 *__restrict__ Asrc;
   {
     const int am = lane & 15;
     const int aa = tx * XB + wave * MF_G + (am >> 2);
-    Asrc = p.FX + (long long)(aa < p.n1 ? aa : p.n1 - 1) * q.rx + (am & 3) * KP + (lane >> 4) * KQ;
+    Asrc = reinterpret_cast<const _Float16 *>(p.FX + (long long)(aa < p.n1 ? aa : p.n1 - 1) * q.rx +
+                                              mf_half_off(q.d, p.l1)) + (am & 3) * KH + 8 * (lane >> 4);
   }
-  const float *__restrict__ Bl = Bs + (lane & 15) * LDB + (lane >> 4) * QS;
+  const long long ALO = (long long)q.rowsx * KH;  // hi rows -> lo rows (halves)
+  const _Float16 *__restrict__ Bl = Bs + (lane & 15) * LDBH + 8 * (lane >> 4);
+  // D rows of lane l belong to x-sequence l >> 4: 2^-(e_a + e_b) undoes both scales (exact)
+  float dsc;
+  {
+    const int aw = tx * XB + wave * MF_G + (lane >> 4);
+    dsc = rsy * p.FX[(long long)(aw < p.n1 ? aw : p.n1 - 1) * q.rx + mf_scale_off(q.d, p.l1)];
+  }
   // the last tile column holds <dx_i, y_{j0}>: its writers subtract g_i there, so the tile carries p_{i,j0}
   const float *__restrict__ ggw;
   {
@@ -211,27 +241,21 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4)
     f4 acc[NCB];
 #pragma unroll
     for (int cb = 0; cb < NCB; ++cb) acc[cb] = (f4){0.0f, 0.0f, 0.0f, 0.0f};
-    const float *__restrict__ ap = Asrc + (long long)ch * 4 * KP;
-    f2 an[4];
+    const _Float16 *__restrict__ ap = Asrc + (long long)ch * 4 * KH;
+    h8 nhi = *reinterpret_cast<const h8 *>(ap), nlo = *reinterpret_cast<const h8 *>(ap + ALO);
+    for (int s = 0; s < KH; s += 32) {
+      const h8 ahi = nhi, alo = nlo;
+      if (s + 32 < KH) {
+        nhi = *reinterpret_cast<const h8 *>(ap + s + 32);
+        nlo = *reinterpret_cast<const h8 *>(ap + ALO + s + 32);
+      }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) an[u] = 2 * u < KQ ? *reinterpret_cast<const f2 *>(ap + 2 * u) : (f2){0.0f, 0.0f};
-    for (int s = 0; s < KQ; s += 8) {
-      f2 ac[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) ac[u] = an[u];
-#pragma unroll
-      for (int u = 0; u < 4; ++u)
-        an[u] = s + 8 + 2 * u < KQ ? *reinterpret_cast<const f2 *>(ap + s + 8 + 2 * u) : (f2){0.0f, 0.0f};
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (s + 2 * u < KQ) {
-#pragma unroll
-          for (int cb = 0; cb < NCB; ++cb) {
-            const f2 bv = *reinterpret_cast<const f2 *>(Bl + cb * 16 * LDB + s + 2 * u);
-            acc[cb] = mfma16(ac[u][0], bv[0], acc[cb]);
-            acc[cb] = mfma16(ac[u][1], bv[1], acc[cb]);
-          }
-        }
+      for (int cb = 0; cb < NCB; ++cb) {
+        const h8 bhi = *reinterpret_cast<const h8 *>(Bl + cb * 16 * LDBH + s);
+        const h8 blo = *reinterpret_cast<const h8 *>(Bl + cb * 16 * LDBH + KH + s);
+        acc[cb] = mfma16h(alo, bhi, acc[cb]);
+        acc[cb] = mfma16h(ahi, blo, acc[cb]);
+        acc[cb] = mfma16h(ahi, bhi, acc[cb]);
       }
     }
     wave_lds_sync();  // the previous chunk's rows are read
@@ -244,7 +268,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4)
       float *__restrict__ crow = Cs + (4 * r + gq) * LDC + col;
 #pragma unroll
       for (int cb = 0; cb < NCB; ++cb) {
-        float v = acc[cb][r];
+        float v = acc[cb][r] * dsc;
         if (cb == NCB - 1 && col == 15 && t >= 1 && t - 1 < nrows) v -= ggw[t - 1];
         crow[16 * cb] = v;
       }
@@ -333,7 +357,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4)
       // lanes splitting the channels
       float s00 = 0.0f;
       for (int k = gl; k < q.d; k += LP) {
-        const float df = fx[k] - Bs[(LPW - 1) * LDB + (k / KQ) * QS + k % KQ];
+        const float df = fx[k] - pty[(long long)j0 * KP + k];
         s00 = __builtin_fmaf(df, df, s00);
       }
       const float e00 = -0.5f * group_sum<LP>(s00);

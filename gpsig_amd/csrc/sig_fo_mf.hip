@@ -52,10 +52,63 @@ __global__ __launch_bounds__(256) void mf_scalars_kernel(const float *__restrict
   base[rows + i] = (i + 1 < l) ? (float)(gx + 0.5 * (double)h) : 0.0f;
 }
 
+// The sequence's scale 2^e (sig_fo_mf.h mf_split): its largest |point| or |increment| to [2^13, 2^14); one
+// workgroup per sequence.  Stores 2^-e, 2^e.
+__global__ __launch_bounds__(256) void mf_scale_kernel(const float *__restrict__ X, int n, int l, int d,
+                                                       float *__restrict__ R) {
+  const int s = (int)blockIdx.x;
+  const float *__restrict__ x = X + (long long)s * l * d;
+  float mx = 0.0f;
+  for (int e = (int)threadIdx.x; e < l * d; e += 256) {
+    const float v = x[e];
+    mx = __builtin_fmaxf(mx, __builtin_fabsf(v));
+    if (e >= d) mx = __builtin_fmaxf(mx, __builtin_fabsf(v - x[e - d]));
+  }
+  __shared__ float red[4];
+  mx = wave_max(mx);
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    mx = __builtin_fmaxf(__builtin_fmaxf(red[0], red[1]), __builtin_fmaxf(red[2], red[3]));
+    int ex = 0;
+    if (mx > 0.0f && __builtin_isfinite(mx)) frexpf(mx, &ex);  // mx in [2^(ex-1), 2^ex)
+    int e = mx > 0.0f && __builtin_isfinite(mx) ? 14 - ex : 0;
+    e = e < -120 ? -120 : (e > 120 ? 120 : e);
+    float *sc = R + (long long)s * mf_rec_floats(d, l) + mf_scale_off(d, l);
+    sc[0] = ldexpf(1.0f, -e);
+    sc[1] = ldexpf(1.0f, e);
+    sc[2] = 0.0f;
+    sc[3] = 0.0f;
+  }
+}
+
+// aug rows as hi / lo halves at the sequence's scale (zero past KP)
+__global__ __launch_bounds__(256) void mf_half_kernel(int n, int l, int d, float *__restrict__ R) {
+  const int rows = mf_rows(l), kp = mf_kp(d), kh = mf_kh(d);
+  const long long rec = mf_rec_floats(d, l);
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long long)n * rows * (kh / 2)) return;
+  const int k = 2 * (int)(idx % (kh / 2));
+  const long long r = idx / (kh / 2);
+  const int t = (int)(r % rows);
+  const int s = (int)(r / rows);
+  float *__restrict__ base = R + (long long)s * rec;
+  const float sc = base[mf_scale_off(d, l) + 1];
+  const f2 v = k < kp ? *reinterpret_cast<const f2 *>(base + (long long)t * kp + k) : (f2){0.0f, 0.0f};
+  const h2 s0 = mf_split(v[0], sc), s1 = mf_split(v[1], sc);
+  _Float16 *__restrict__ hh = reinterpret_cast<_Float16 *>(base + mf_half_off(d, l)) + (long long)t * kh + k;
+  *reinterpret_cast<h2 *>(hh) = (h2){s0[0], s1[0]};
+  *reinterpret_cast<h2 *>(hh + (long long)rows * kh) = (h2){s0[1], s1[1]};
+}
+
 int mf_records(const float *X, int n, int l, int d, float *R, hipStream_t s) {
+  if (n <= 0) return GPSIG_OK;
   const long long ta = (long long)n * mf_rows(l) * mf_kp(d), ts = (long long)n * mf_rows(l);
+  const long long th = (long long)n * mf_rows(l) * (mf_kh(d) / 2);
   hipLaunchKernelGGL(mf_aug_kernel, dim3((unsigned)((ta + 255) / 256)), dim3(256), 0, s, X, n, l, d, R);
   hipLaunchKernelGGL(mf_scalars_kernel, dim3((unsigned)((ts + 255) / 256)), dim3(256), 0, s, X, n, l, d, R);
+  hipLaunchKernelGGL(mf_scale_kernel, dim3((unsigned)n), dim3(256), 0, s, X, n, l, d, R);
+  hipLaunchKernelGGL(mf_half_kernel, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, s, n, l, d, R);
   return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
 }
 
