@@ -40,16 +40,18 @@ __host__ __device__ inline int mf_kq(int d) {
   return q + (q & 1);
 }
 __host__ __device__ inline int mf_kp(int d) { return 4 * mf_kq(d); }
-// The GEMM runs on v_mfma_f32_16x16x32_f16 with every fp32 operand split into two halves, a = 2^-e (hi + lo)
-// (hi = f16(2^e a), lo = f16(2^e a - hi), 2^e per sequence putting its largest |value| in [2^13, 2^14)):
-// hi hi' + hi lo' + lo hi' carries 22 of the 24 mantissa bits (products exact in the fp32 accumulator), the
-// same error as the fp32 dot it replaces (|err| / sum |terms| 2.3e-7 vs 2.0e-7 on random walks, d = 46), at a
-// sixteenth of the f32 MFMA's cycles per product (16 cycles per 16x16x32 against 32 per 16x16x4): 3 passes,
-// 5.3x fewer matrix-core cycles.  K is padded to KH = 32 multiples.
+// The GEMM runs on v_mfma_f32_16x16x32_f16 with every fp32 operand split into NP halves at a power-of-two
+// scale, a = 2^-e (h_0 + h_1 [+ h_2]), h_u = f16 of what the previous parts left: the products h_u h'_v with
+// u + v < NP carry 22 (NP = 2) or 33 (NP = 3) bits of every product, exact in the fp32 accumulator (16
+// cycles per 16x16x32 against 32 per 16x16x4 for the f32 form: 3 or 6 MFMAs per 32 channels instead of 8).
+// The scales keep the low parts above the f16 subnormal range, which the matrix cores flush: the A rows (x_0,
+// dx_t) each at their own 2^e (largest |component| in [2^14, 2^15)), the B side at one scale for y's
+// increments and one for its points.  K is padded to KH = 32 multiples.
 __host__ __device__ inline int mf_kh(int d) { return (d + 31) & ~31; }
-// B image in LDS: column j at j LDBH halves, [hi: KH][lo: KH] + 8 halves of padding (a column stride of
-// 68 mod 64 dwords: the 16 columns of a ds_read_b128 start on distinct 4-bank groups)
-__host__ __device__ inline int mf_ldbh(int d) { return 2 * mf_kh(d) + 8; }
+constexpr int MF_NPMAX = 3;
+// B image in LDS: column j at j LDBH halves, parts u at u KH, + 8 halves of padding (a column stride of
+// 4 mod 16 dwords for every KH: the 16 columns of a ds_read_b128 start on distinct 4-bank groups)
+__host__ __device__ inline int mf_ldbh(int d, int np) { return np * mf_kh(d) + 8; }
 // columns per lane by sequence length: one tile of LP W columns up to 160 points, past that W = 8 in column
 // blocks of LPW - 1 = 127 cells (the block's last column is the point of its first cell, below)
 __host__ __device__ inline int mf_w(int l) { return l <= 64 ? 4 : (l <= 128 ? 8 : (l <= 160 ? 10 : 8)); }
@@ -61,27 +63,43 @@ __host__ __device__ inline int mf_rows(int l) {
   const int r = (l + 3) & ~3, w = mf_lpw(l);
   return r > w ? r : w;
 }
-// record of a sequence (floats): [aug: rows x KP][points: rows x KP][hd: rows][gg: rows][2^-e, 2^e, 0, 0]
-// [aug hi: rows x KH halves][aug lo: rows x KH halves]
+// record of a sequence (floats): [aug: rows x KP][points: rows x KP][hd: rows][gg: rows]
+// [B scales: 2^-e_inc, 2^e_inc, 2^-e_pt, 2^e_pt][A row scales: 2^-e_t (rows), 2^e_t (rows)]
+// [aug parts u = 0..2: rows x KH halves each]
 //   aug row 0 = x_0, aug row t = x_t - x_{t-1} (1 <= t < l), points row t = x_t; zero past l and past d
 //   (every section 16-byte aligned: rows is a multiple of 4, KP of 8, KH of 32)
 __host__ __device__ inline long long mf_scale_off(int d, int l) { return 2LL * mf_rows(l) * mf_kp(d) + 2LL * mf_rows(l); }
-__host__ __device__ inline long long mf_half_off(int d, int l) { return mf_scale_off(d, l) + 4; }
+__host__ __device__ inline long long mf_rowsc_off(int d, int l) { return mf_scale_off(d, l) + 4; }
+__host__ __device__ inline long long mf_half_off(int d, int l) { return mf_rowsc_off(d, l) + 2LL * mf_rows(l); }
 __host__ __device__ inline long long mf_rec_floats(int d, int l) {
-  return mf_half_off(d, l) + (long long)mf_rows(l) * mf_kh(d);
+  return mf_half_off(d, l) + (long long)mf_rows(l) * mf_kh(d) * MF_NPMAX / 2;
 }
-inline size_t mf_lds_bytes(int d, int l2, int nw) {
+inline size_t mf_lds_bytes(int d, int l2, int nw, int np) {
   const size_t lpw = (size_t)mf_lpw(l2);
-  return lpw * (size_t)mf_ldbh(d) * 2 + (size_t)nw * 16 * (lpw + 4) * sizeof(float);
+  return lpw * (size_t)mf_ldbh(d, np) * 2 + (size_t)nw * 16 * (lpw + 4) * sizeof(float);
 }
-// waves per workgroup: 8 (two per SIMD, so one wave's matrix-core phase overlaps another's recursion) when
-// the LDS allows, else 4 (wide B images: d > 114 at 129..160 points); 0: no tile geometry
-inline int mf_waves(int d, int l2) {
-  if (mf_w(l2) == 0) return 0;
-  static const bool four = [] { const char *e = getenv("GPSIG_MF_NW"); return e && e[0] == '4'; }();  // A/B
-  if (!four && mf_lds_bytes(d, l2, 8) <= MF_LDS_MAX) return 8;
-  return mf_lds_bytes(d, l2, 4) <= MF_LDS_MAX ? 4 : 0;
+// Launch geometry by LDS: 8 waves per workgroup (two per SIMD, so one wave's matrix-core phase overlaps
+// another's recursion) when the LDS allows, else 4; 0: no tile geometry.  Operand parts: 2 (22 bits); with
+// GPSIG_MF_PARTS=3 three (33 bits) where the B image fits.  The third part buys little: the matrix cores align
+// a product block to its largest term and truncate below it (tools/mfma_f16_probe.hip: -0.52 ulp mean on
+// positive terms spread over 2^8), which the recurrences' running sums then accumulate; per-level error vs
+// fp64 1.0-1.2e-6 (2 parts) against 0.9-1.1e-6 (3 parts) at 500 points, 1.2-1.5e-7 for the fp32 channel loop
+// (GPSIG_WIDE_MF=0), at 1.2x the time.  GPSIG_MF_NW=4 pins 4 waves (A/B runs).
+struct MfGeo {
+  int nw, np;
+};
+inline MfGeo mf_geo(int d, int l2) {
+  if (mf_w(l2) == 0) return {0, 0};
+  static const int parts = [] { const char *e = getenv("GPSIG_MF_PARTS"); return e ? atoi(e) : 2; }();
+  static const bool four = [] { const char *e = getenv("GPSIG_MF_NW"); return e && e[0] == '4'; }();
+  for (int nw : {8, 4}) {
+    if (nw == 8 && four) continue;
+    if (parts == 3 && mf_lds_bytes(d, l2, nw, 3) <= MF_LDS_MAX) return {nw, 3};
+    if (mf_lds_bytes(d, l2, nw, 2) <= MF_LDS_MAX) return {nw, 2};
+  }
+  return {0, 0};
 }
+inline int mf_waves(int d, int l2) { return mf_geo(d, l2).nw; }
 inline bool mf_applies(int d, int l2) { return mf_waves(d, l2) != 0; }
 
 struct MfArgs {
@@ -109,11 +127,21 @@ typedef _Float16 h2 __attribute__((ext_vector_type(2)));
 // v_mfma_f32_16x16x32_f16: lane l supplies A[l & 15][8 (l >> 4) + e] and B[8 (l >> 4) + e][l & 15], e < 8;
 // D row 4 (l >> 4) + r, col l & 15
 GPSIG_DEV f4 mfma16h(h8 a, h8 b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0); }
-// v = 2^-e (hi + lo) at the sequence's scale 2^e
-GPSIG_DEV h2 mf_split(float v, float sc) {
-  const float b = v * sc;
-  const _Float16 hi = (_Float16)b;
-  return (h2){hi, (_Float16)(b - (float)hi)};
+// v = 2^-e (h_0 + ... + h_{NP-1}) at the scale 2^e
+template <int NP>
+struct MfParts {
+  _Float16 h[NP];
+};
+template <int NP>
+GPSIG_DEV MfParts<NP> mf_split(float v, float sc) {
+  MfParts<NP> r;
+  float b = v * sc;
+#pragma unroll
+  for (int u = 0; u < NP; ++u) {
+    r.h[u] = (_Float16)b;
+    b -= (float)r.h[u];
+  }
+  return r;
 }
 
 // Wavefront-scope ordering of the wave's own LDS tile between its lanes (writes by one lane, reads by another)
@@ -123,7 +151,7 @@ GPSIG_DEV void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-template <int NW, int W, int M, int SEED, bool SAVE, bool BLK, bool DMO = false>
+template <int NW, int W, int M, int SEED, bool SAVE, bool BLK, bool DMO = false, int NP = 3>
 __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4))) void sig_fo_mf_kernel(MfArgs q) {
   static_assert(SEED == SEED_RBF_DIFF || SEED == SEED_LIN_DIFF, "difference seeds");
   static_assert(!BLK || W == 8, "column blocks at W = 8");
@@ -137,7 +165,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4)
   constexpr int CPB = LPW - 1;   // cells per column block
   const SigArgs &p = q.p;
   extern __shared__ __attribute__((aligned(16))) float mf_lds[];
-  const int KP = q.kp, KH = mf_kh(q.d), LDBH = 2 * KH + 8;
+  const int KP = q.kp, KH = mf_kh(q.d), LDBH = NP * KH + 8;
   _Float16 *__restrict__ Bs = reinterpret_cast<_Float16 *>(mf_lds);
   const int lane = (int)threadIdx.x & 63;
   const int wave = wave_uniform((int)threadIdx.x >> 6);
@@ -162,7 +190,9 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4)
   }
   const float *__restrict__ fyb = p.FY + (long long)b * q.ry;
   const float *__restrict__ pty = fyb + (long long)q.rowsy * KP;  // y's points
-  const float sy = fyb[mf_scale_off(q.d, p.l2) + 1], rsy = fyb[mf_scale_off(q.d, p.l2)];  // 2^e_b, 2^-e_b
+  // y's scales: increments (B columns < LPW - 1) and points (the last column)
+  const float *__restrict__ ysc = fyb + mf_scale_off(q.d, p.l2);
+  const float syi = ysc[1], syp = ysc[3], rsyi = ysc[0], rsyp = ysc[2];
   // B image of column block j0: column jj < LPW - 1 = aug row j0 + jj + 1 (dy_{j0+jj}), column LPW - 1 = the
   // point y_{j0}, split into halves at y's scale: column j at j LDBH, hi at k, lo at KH + k
   auto load_b = [&](int j0) {
@@ -171,9 +201,10 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4)
       const int j = e / k2n, k = 2 * (e - j * k2n);
       const float *src = j + 1 == LPW ? pty + (long long)j0 * KP : fyb + (long long)(j0 + j + 1) * KP;
       const f2 v = k < KP ? *reinterpret_cast<const f2 *>(src + k) : (f2){0.0f, 0.0f};
-      const h2 s0 = mf_split(v[0], sy), s1 = mf_split(v[1], sy);
-      *reinterpret_cast<h2 *>(Bs + j * LDBH + k) = (h2){s0[0], s1[0]};
-      *reinterpret_cast<h2 *>(Bs + j * LDBH + KH + k) = (h2){s0[1], s1[1]};
+      const float sy = j + 1 == LPW ? syp : syi;
+      const MfParts<NP> s0 = mf_split<NP>(v[0], sy), s1 = mf_split<NP>(v[1], sy);
+#pragma unroll
+      for (int u = 0; u < NP; ++u) *reinterpret_cast<h2 *>(Bs + j * LDBH + u * KH + k) = (h2){s0.h[u], s1.h[u]};
     }
   };
   load_b(0);
@@ -205,13 +236,13 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4)
     Asrc = reinterpret_cast<const _Float16 *>(p.FX + (long long)(aa < p.n1 ? aa : p.n1 - 1) * q.rx +
                                               mf_half_off(q.d, p.l1)) + (am & 3) * KH + 8 * (lane >> 4);
   }
-  const long long ALO = (long long)q.rowsx * KH;  // hi rows -> lo rows (halves)
+  const long long ALO = (long long)q.rowsx * KH;  // part u of the rows at u ALO (halves)
   const _Float16 *__restrict__ Bl = Bs + (lane & 15) * LDBH + 8 * (lane >> 4);
-  // D rows of lane l belong to x-sequence l >> 4: 2^-(e_a + e_b) undoes both scales (exact)
-  float dsc;
+  // D rows of lane l are rows 4 ch + r of x-sequence l >> 4: 2^-(e_row + e_col) undoes both scales (exact)
+  const float *__restrict__ xrs;
   {
     const int aw = tx * XB + wave * MF_G + (lane >> 4);
-    dsc = rsy * p.FX[(long long)(aw < p.n1 ? aw : p.n1 - 1) * q.rx + mf_scale_off(q.d, p.l1)];
+    xrs = p.FX + (long long)(aw < p.n1 ? aw : p.n1 - 1) * q.rx + mf_rowsc_off(q.d, p.l1);
   }
   // the last tile column holds <dx_i, y_{j0}>: its writers subtract g_i there, so the tile carries p_{i,j0}
   const float *__restrict__ ggw;
@@ -242,20 +273,28 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4)
 #pragma unroll
     for (int cb = 0; cb < NCB; ++cb) acc[cb] = (f4){0.0f, 0.0f, 0.0f, 0.0f};
     const _Float16 *__restrict__ ap = Asrc + (long long)ch * 4 * KH;
-    h8 nhi = *reinterpret_cast<const h8 *>(ap), nlo = *reinterpret_cast<const h8 *>(ap + ALO);
+    const f4 rsc = *reinterpret_cast<const f4 *>(xrs + 4 * ch);  // 2^-e of the chunk's 4 rows
+    h8 na[NP];
+#pragma unroll
+    for (int u = 0; u < NP; ++u) na[u] = *reinterpret_cast<const h8 *>(ap + u * ALO);
     for (int s = 0; s < KH; s += 32) {
-      const h8 ahi = nhi, alo = nlo;
+      h8 av[NP];
+#pragma unroll
+      for (int u = 0; u < NP; ++u) av[u] = na[u];
       if (s + 32 < KH) {
-        nhi = *reinterpret_cast<const h8 *>(ap + s + 32);
-        nlo = *reinterpret_cast<const h8 *>(ap + ALO + s + 32);
+#pragma unroll
+        for (int u = 0; u < NP; ++u) na[u] = *reinterpret_cast<const h8 *>(ap + u * ALO + s + 32);
       }
 #pragma unroll
       for (int cb = 0; cb < NCB; ++cb) {
-        const h8 bhi = *reinterpret_cast<const h8 *>(Bl + cb * 16 * LDBH + s);
-        const h8 blo = *reinterpret_cast<const h8 *>(Bl + cb * 16 * LDBH + KH + s);
-        acc[cb] = mfma16h(alo, bhi, acc[cb]);
-        acc[cb] = mfma16h(ahi, blo, acc[cb]);
-        acc[cb] = mfma16h(ahi, bhi, acc[cb]);
+        h8 bv[NP];
+#pragma unroll
+        for (int u = 0; u < NP; ++u) bv[u] = *reinterpret_cast<const h8 *>(Bl + cb * 16 * LDBH + u * KH + s);
+        // the products of parts u + v < NP, smallest first: (lo, hi), (hi, lo) [, (mid, mid) ...], (hi, hi)
+#pragma unroll
+        for (int t = NP - 1; t >= 0; --t)
+#pragma unroll
+          for (int u = t; u >= 0; --u) acc[cb] = mfma16h(av[u], bv[t - u], acc[cb]);
       }
     }
     wave_lds_sync();  // the previous chunk's rows are read
@@ -268,7 +307,7 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4)
       float *__restrict__ crow = Cs + (4 * r + gq) * LDC + col;
 #pragma unroll
       for (int cb = 0; cb < NCB; ++cb) {
-        float v = acc[cb][r] * dsc;
+        float v = acc[cb][r] * (rsc[r] * (cb == NCB - 1 && col == 15 ? rsyp : rsyi));
         if (cb == NCB - 1 && col == 15 && t >= 1 && t - 1 < nrows) v -= ggw[t - 1];
         crow[16 * cb] = v;
       }

@@ -52,37 +52,65 @@ __global__ __launch_bounds__(256) void mf_scalars_kernel(const float *__restrict
   base[rows + i] = (i + 1 < l) ? (float)(gx + 0.5 * (double)h) : 0.0f;
 }
 
-// The sequence's scale 2^e (sig_fo_mf.h mf_split): its largest |point| or |increment| to [2^13, 2^14); one
-// workgroup per sequence.  Stores 2^-e, 2^e.
+// 2^e with the largest |value| m at 2^e m in [2^14, 2^15) (1 for m = 0), as 2^-e, 2^e
+GPSIG_DEV f2 mf_scale_of(float m) {
+  int ex = 0;
+  if (m > 0.0f && __builtin_isfinite(m)) frexpf(m, &ex);  // m in [2^(ex-1), 2^ex)
+  int e = m > 0.0f && __builtin_isfinite(m) ? 15 - ex : 0;
+  e = e < -120 ? -120 : (e > 120 ? 120 : e);
+  return (f2){ldexpf(1.0f, -e), ldexpf(1.0f, e)};
+}
+
+// The B-side scales of a sequence (sig_fo_mf.h): its largest |increment| and its largest |point|; one
+// workgroup per sequence.
 __global__ __launch_bounds__(256) void mf_scale_kernel(const float *__restrict__ X, int n, int l, int d,
                                                        float *__restrict__ R) {
   const int s = (int)blockIdx.x;
   const float *__restrict__ x = X + (long long)s * l * d;
-  float mx = 0.0f;
+  float mi = 0.0f, mp = 0.0f;
   for (int e = (int)threadIdx.x; e < l * d; e += 256) {
     const float v = x[e];
-    mx = __builtin_fmaxf(mx, __builtin_fabsf(v));
-    if (e >= d) mx = __builtin_fmaxf(mx, __builtin_fabsf(v - x[e - d]));
+    mp = __builtin_fmaxf(mp, __builtin_fabsf(v));
+    if (e >= d) mi = __builtin_fmaxf(mi, __builtin_fabsf(v - x[e - d]));
   }
-  __shared__ float red[4];
-  mx = wave_max(mx);
-  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __shared__ float red[2][4];
+  mi = wave_max(mi);
+  mp = wave_max(mp);
+  if ((threadIdx.x & 63) == 0) {
+    red[0][threadIdx.x >> 6] = mi;
+    red[1][threadIdx.x >> 6] = mp;
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
-    mx = __builtin_fmaxf(__builtin_fmaxf(red[0], red[1]), __builtin_fmaxf(red[2], red[3]));
-    int ex = 0;
-    if (mx > 0.0f && __builtin_isfinite(mx)) frexpf(mx, &ex);  // mx in [2^(ex-1), 2^ex)
-    int e = mx > 0.0f && __builtin_isfinite(mx) ? 14 - ex : 0;
-    e = e < -120 ? -120 : (e > 120 ? 120 : e);
+    mi = __builtin_fmaxf(__builtin_fmaxf(red[0][0], red[0][1]), __builtin_fmaxf(red[0][2], red[0][3]));
+    mp = __builtin_fmaxf(__builtin_fmaxf(red[1][0], red[1][1]), __builtin_fmaxf(red[1][2], red[1][3]));
     float *sc = R + (long long)s * mf_rec_floats(d, l) + mf_scale_off(d, l);
-    sc[0] = ldexpf(1.0f, -e);
-    sc[1] = ldexpf(1.0f, e);
-    sc[2] = 0.0f;
-    sc[3] = 0.0f;
+    const f2 a = mf_scale_of(mi), b = mf_scale_of(mp);
+    sc[0] = a[0];
+    sc[1] = a[1];
+    sc[2] = b[0];
+    sc[3] = b[1];
   }
 }
 
-// aug rows as hi / lo halves at the sequence's scale (zero past KP)
+// The A-side scale of every aug row (x_0, dx_t; 1 past the sequence), after mf_aug_kernel
+__global__ __launch_bounds__(256) void mf_rowscale_kernel(int n, int l, int d, float *__restrict__ R) {
+  const int rows = mf_rows(l), kp = mf_kp(d);
+  const long long idx = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (idx >= (long long)n * rows) return;
+  const int t = (int)(idx % rows);
+  const int s = (int)(idx / rows);
+  float *__restrict__ base = R + (long long)s * mf_rec_floats(d, l);
+  const float *__restrict__ row = base + (long long)t * kp;
+  float m = 0.0f;
+  for (int k = 0; k < d; ++k) m = __builtin_fmaxf(m, __builtin_fabsf(row[k]));
+  const f2 sc = mf_scale_of(m);
+  float *__restrict__ rs = base + mf_rowsc_off(d, l);
+  rs[t] = sc[0];
+  rs[rows + t] = sc[1];
+}
+
+// aug rows as MF_NPMAX halves at their row scale (zero past KP); a kernel with 2 parts reads the first two
 __global__ __launch_bounds__(256) void mf_half_kernel(int n, int l, int d, float *__restrict__ R) {
   const int rows = mf_rows(l), kp = mf_kp(d), kh = mf_kh(d);
   const long long rec = mf_rec_floats(d, l);
@@ -93,12 +121,12 @@ __global__ __launch_bounds__(256) void mf_half_kernel(int n, int l, int d, float
   const int t = (int)(r % rows);
   const int s = (int)(r / rows);
   float *__restrict__ base = R + (long long)s * rec;
-  const float sc = base[mf_scale_off(d, l) + 1];
+  const float sc = base[mf_rowsc_off(d, l) + rows + t];
   const f2 v = k < kp ? *reinterpret_cast<const f2 *>(base + (long long)t * kp + k) : (f2){0.0f, 0.0f};
-  const h2 s0 = mf_split(v[0], sc), s1 = mf_split(v[1], sc);
+  const MfParts<MF_NPMAX> s0 = mf_split<MF_NPMAX>(v[0], sc), s1 = mf_split<MF_NPMAX>(v[1], sc);
   _Float16 *__restrict__ hh = reinterpret_cast<_Float16 *>(base + mf_half_off(d, l)) + (long long)t * kh + k;
-  *reinterpret_cast<h2 *>(hh) = (h2){s0[0], s1[0]};
-  *reinterpret_cast<h2 *>(hh + (long long)rows * kh) = (h2){s0[1], s1[1]};
+#pragma unroll
+  for (int u = 0; u < MF_NPMAX; ++u) *reinterpret_cast<h2 *>(hh + (long long)u * rows * kh) = (h2){s0.h[u], s1.h[u]};
 }
 
 int mf_records(const float *X, int n, int l, int d, float *R, hipStream_t s) {
@@ -108,6 +136,7 @@ int mf_records(const float *X, int n, int l, int d, float *R, hipStream_t s) {
   hipLaunchKernelGGL(mf_aug_kernel, dim3((unsigned)((ta + 255) / 256)), dim3(256), 0, s, X, n, l, d, R);
   hipLaunchKernelGGL(mf_scalars_kernel, dim3((unsigned)((ts + 255) / 256)), dim3(256), 0, s, X, n, l, d, R);
   hipLaunchKernelGGL(mf_scale_kernel, dim3((unsigned)n), dim3(256), 0, s, X, n, l, d, R);
+  hipLaunchKernelGGL(mf_rowscale_kernel, dim3((unsigned)((ts + 255) / 256)), dim3(256), 0, s, n, l, d, R);
   hipLaunchKernelGGL(mf_half_kernel, dim3((unsigned)((th + 255) / 256)), dim3(256), 0, s, n, l, d, R);
   return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
 }

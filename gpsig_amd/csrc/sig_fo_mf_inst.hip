@@ -8,14 +8,21 @@
 
 namespace gpsig {
 
+template <int NW, int W, int M, int SEED, bool BLK, int NP>
+static int mf_launch_np(const MfArgs &a, long long nblocks, hipStream_t s) {
+  const size_t lds = mf_lds_bytes(a.d, a.p.l2, NW, NP);
+  if (a.p.state)
+    hipLaunchKernelGGL((sig_fo_mf_kernel<NW, W, M, SEED, true, BLK, false, NP>), dim3((unsigned)nblocks), dim3(64 * NW), lds,
+                       s, a);
+  else
+    hipLaunchKernelGGL((sig_fo_mf_kernel<NW, W, M, SEED, false, BLK, false, NP>), dim3((unsigned)nblocks), dim3(64 * NW), lds,
+                       s, a);
+  return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
+}
 template <int NW, int W, int M, int SEED, bool BLK>
 static int mf_launch_blk(const MfArgs &a, long long nblocks, hipStream_t s) {
-  const size_t lds = mf_lds_bytes(a.d, a.p.l2, NW);
-  if (a.p.state)
-    hipLaunchKernelGGL((sig_fo_mf_kernel<NW, W, M, SEED, true, BLK>), dim3((unsigned)nblocks), dim3(64 * NW), lds, s, a);
-  else
-    hipLaunchKernelGGL((sig_fo_mf_kernel<NW, W, M, SEED, false, BLK>), dim3((unsigned)nblocks), dim3(64 * NW), lds, s, a);
-  return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
+  return mf_geo(a.d, a.p.l2).np == 3 ? mf_launch_np<NW, W, M, SEED, BLK, 3>(a, nblocks, s)
+                                     : mf_launch_np<NW, W, M, SEED, BLK, 2>(a, nblocks, s);
 }
 template <int NW, int W, int M, int SEED>
 static int mf_launch_nw(const MfArgs &a, long long nblocks, hipStream_t s) {
@@ -61,12 +68,16 @@ int sig_fo_mf_launch_m<GPSIG_M>(const MfArgs &a, int seed, long long nblocks, hi
 
 #if GPSIG_M == 1
 // The RBF cells of a chunk of pairs into the higher-order recursion's tile (DMO instantiations).
+template <int NW, int W, bool BLK, int NP>
+static int mf_cells_np(const MfArgs &a, long long nblocks, hipStream_t s) {
+  const size_t lds = mf_lds_bytes(a.d, a.p.l2, NW, NP);
+  hipLaunchKernelGGL((sig_fo_mf_kernel<NW, W, 1, SEED_RBF_DIFF, false, BLK, true, NP>), dim3((unsigned)nblocks),
+                     dim3(64 * NW), lds, s, a);
+  return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
+}
 template <int NW, int W, bool BLK>
 static int mf_cells_launch(const MfArgs &a, long long nblocks, hipStream_t s) {
-  const size_t lds = mf_lds_bytes(a.d, a.p.l2, NW);
-  hipLaunchKernelGGL((sig_fo_mf_kernel<NW, W, 1, SEED_RBF_DIFF, false, BLK, true>), dim3((unsigned)nblocks), dim3(64 * NW),
-                     lds, s, a);
-  return hipGetLastError() == hipSuccess ? GPSIG_OK : GPSIG_ELAUNCH;
+  return mf_geo(a.d, a.p.l2).np == 3 ? mf_cells_np<NW, W, BLK, 3>(a, nblocks, s) : mf_cells_np<NW, W, BLK, 2>(a, nblocks, s);
 }
 template <int NW>
 static int mf_cells_nw(const MfArgs &a, long long nblocks, hipStream_t s) {
