@@ -759,6 +759,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
       // this lane's LDS slots, then consumed in reverse.  Cells with |p| or |c| >= EM1_TAU take the
       // corner difference of the k grid with an exact next row (wave-uniform branch).
       float(*cb)[64][2 * W] = cbuf[wave];
+      // |c_ij| <= 2 sqrt(hdx_i hdy_j): when the bound over the wave's rows and columns allows, Ec takes the
+      // forward's cubic and only the first column's p meets a polynomial (the others follow the exact chain
+      // Ep' = Ep + (1 + Ep) Ec), as RbfSeedPk::row's CLO rows
+      bool clo = false;
+      {
+        float hx = 0.0f, hy = 0.0f;
+        for (int i = lane; i < nrows; i += 64) hx = __builtin_fmaxf(hx, fxc[(long long)i * FS + 2 * DP]);
+#pragma unroll
+        for (int w = 0; w < W; ++w) hy = __builtin_fmaxf(hy, hdy[w]);
+        hx = wave_max(hx);
+        hy = wave_max(hy);
+        clo = wave_uniform(4.0f * hx * hy < 0.98f * EM1_LO_TAU * EM1_LO_TAU ? 1 : 0) != 0;
+      }
+      auto em1_cubic = [](float x) {
+        float q = __builtin_fmaf(4.166666667e-02f, x, 1.666992186e-01f);
+        q = __builtin_fmaf(q, x, 5.000000132e-01f);
+        q = __builtin_fmaf(q, x, 9.999999841e-01f);
+        return q * x;
+      };
       auto exact_row = [&](cfloat *xr, float (&k)[W], float (&Eq)[W]) {
         float xv[DP];
 #pragma unroll
@@ -776,7 +795,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
           Eq[w] = __builtin_fabsf(q) < EM1_TAU ? em1_small(q) : __builtin_amdgcn_exp2f(q * L2E) - 1.0f;
         }
       };
-      auto chunk_fwd = [&](int i0, int nr) {
+      auto chunk_fwd = [&](auto clo_t, int i0, int nr) {
+        constexpr bool CLO = decltype(clo_t)::value;
         float kc[W], Eq[W];
         exact_row(fxc + (long long)i0 * FS, kc, Eq);
         for (int r = 0; r < nr; ++r) {
@@ -805,7 +825,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
           float Ep = em1_small(pp[0]);
 #pragma unroll
           for (int w = 0; w < W; ++w) {
-            const float c = cv[w], Ec = em1_small(c);
+            const float c = cv[w], Ec = CLO ? em1_cubic(c) : em1_small(c);
             float t = __builtin_fmaf(Ep, Ec, Ec);
             const float Epw = Ep;
             Ep += t;
@@ -813,8 +833,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
             dM[w] = kc[w] * __builtin_fmaf(Epw, Eq[w], t);
             kn[w] = __builtin_fmaf(kc[w], Epw, kc[w]);
             Eqn[w] = __builtin_fmaf(Eq[w], Ec, Eq[w] + Ec);
-            mx[w] = __builtin_fmaxf(__builtin_fabsf(pp[w]), __builtin_fabsf(c));
-            slow = slow || !(mx[w] < EM1_TAU);
+            mx[w] = CLO ? __builtin_fabsf(pp[w]) : __builtin_fmaxf(__builtin_fabsf(pp[w]), __builtin_fabsf(c));
+            if (!CLO || w == 0) slow = slow || !(mx[w] < EM1_TAU);
           }
           if (__builtin_amdgcn_ballot_w64(slow) != 0) {
             // out-of-range cells may have spoilt the chained Ep: in-range cells from their own p
@@ -841,7 +861,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
       };
       for (int i0 = ((nrows - 1) / RC) * RC; i0 >= 0; i0 -= RC) {
         const int nr = nrows - i0 < RC ? nrows - i0 : RC;
-        chunk_fwd(i0, nr);
+        if (clo)
+          chunk_fwd(std::true_type{}, i0, nr);
+        else
+          chunk_fwd(std::false_type{}, i0, nr);
         for (int r = nr - 1; r >= 0; --r) {
           float dM[W], k0[W];
 #pragma unroll

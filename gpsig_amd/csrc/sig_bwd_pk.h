@@ -290,10 +290,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWDPK
         Eqn[w2] = fma2(Eq[w2], Ec[w2], Eq[w2] + Ec[w2]);
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
-          if constexpr (CLO)
-            mx = __builtin_fmaxf(mx, __builtin_fabsf(p2[w2][h]));
-          else
+          if constexpr (CLO) {  // the pairs after the first follow the exact Ep chain (RbfSeedPk::row)
+            if (w2 == 0) mx = __builtin_fmaxf(mx, __builtin_fabsf(p2[w2][h]));
+          } else {
             mx = __builtin_fmaxf(__builtin_fmaxf(mx, __builtin_fabsf(p2[w2][h])), __builtin_fabsf(c2[w2][h]));
+          }
         }
       }
       if (__builtin_amdgcn_ballot_w64(mx >= EM1_TAU) != 0) {

@@ -246,6 +246,9 @@ struct RowSeed {
 #ifndef GPSIG_NAIVE
 #define GPSIG_NAIVE 1
 #endif
+#ifndef GPSIG_P0CHECK
+#define GPSIG_P0CHECK 1
+#endif
 template <int DP, int W>
 struct RbfSeedPk {
   static_assert(W % 2 == 0, "column pairs");
@@ -434,10 +437,13 @@ struct RbfSeedPk {
       dM[w2] = kc[w2] * fma2(Ep[w2], Eq[w2], t2);
 #pragma unroll
       for (int h = 0; h < 2; ++h) {
-        if constexpr (CLO)  // |c| < EM1_LO_TAU < EM1_TAU a priori
-          mx = __builtin_fmaxf(mx, __builtin_fabsf(p[w2][h]));
-        else
+        // CLO: every Ec is in the cubic's range a priori, and the pairs after the first take Ep by the exact
+        // chain Ep' = Ep + (1 + Ep) Ec, so only the first pair's p meets a polynomial
+        if constexpr (CLO) {
+          if (w2 == 0 || !GPSIG_P0CHECK) mx = __builtin_fmaxf(mx, __builtin_fabsf(p[w2][h]));
+        } else {
           mx = __builtin_fmaxf(__builtin_fmaxf(mx, __builtin_fabsf(p[w2][h])), __builtin_fabsf(c[w2][h]));
+        }
       }
     }
     const bool slow = GPSIG_NAIVE && __builtin_amdgcn_ballot_w64(mx >= EM1_TAU) != 0;

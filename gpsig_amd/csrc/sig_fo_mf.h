@@ -486,10 +486,11 @@ __global__ __launch_bounds__(64 * NW) __attribute__((amdgpu_waves_per_eu(NW / 4)
           dM[w2] = kc[w2] * fma2(Ep[w2], Eq[w2], t2);
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
-            if constexpr (CLO)
-              mx = __builtin_fmaxf(mx, __builtin_fabsf(pv[w2][h]));
-            else
+            if constexpr (CLO) {  // only the first pair's p meets a polynomial (RbfSeedPk::row)
+              if (w2 == 0 || !GPSIG_P0CHECK) mx = __builtin_fmaxf(mx, __builtin_fabsf(pv[w2][h]));
+            } else {
               mx = __builtin_fmaxf(__builtin_fmaxf(mx, __builtin_fabsf(pv[w2][h])), __builtin_fabsf(c[w2][h]));
+            }
           }
         }
         // exact state of the next row: e_{i+1} = e_i + p_i, Q_{i+1} = Q_i + c_i
