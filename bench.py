@@ -169,7 +169,7 @@ def main():
                          "launch writes the cells dM to HBM, a consumer streams them through the recursion")
     ap.add_argument("--backend", default="nccl",
                     help="process-group backend (nccl = RCCL; gloo only to rehearse N>1 ranks on one GPU)")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r5_gram_counters.json"),
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r6_gram_counters.json"),
                     help="per-launch HBM bytes of the Gram kernel from a PMC pass (profiles/*.json)")
     ap.add_argument("--check-rows", type=int, default=256,
                     help="rows of the max_abs_err subsample (SURVEY.md 8d: 256 for large N)")
