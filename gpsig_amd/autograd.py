@@ -85,15 +85,15 @@ def _ho_vjp_kernel(cfg, *lengths):
             and all(ops.ho_vjp_supported(l, cfg["num_levels"], cfg["order"], cfg["base"]) for l in lengths))
 
 
-def _word_counts(d, m, device):
-    """(d^m, d) float64: occurrences of each channel in each word of length m (iisignature's first-index-major
-    order: word index = w_1 d^(m-1) + ... + w_m)."""
-    idx = torch.arange(d ** m, device=device)
-    cnt = torch.zeros((d ** m, d), dtype=torch.float64, device=device)
+def _channel_counts(v, d, m):
+    """sum_w v_w n_c(w) for a level-m vector v (d^m, iisignature's first-index-major word order: index = w_1 d^(m-1)
+    + ... + w_m) and n_c(w) the occurrences of channel c in w: per word position, the sums of v over the other
+    positions, added up (no d^m x d count matrix)."""
+    t = v.reshape((d,) * m)
+    out = torch.zeros(d, dtype=v.dtype, device=v.device)
     for k in range(m):
-        digit = (idx // d ** (m - 1 - k)) % d
-        cnt[idx, digit] += 1.0
-    return cnt
+        out += t.sum(dim=tuple(a for a in range(m) if a != k)) if m > 1 else t
+    return out
 
 
 SCALING_FEATURE_BYTES = int(os.environ.get("GPSIG_SCALING_FEATURE_BYTES", 1 << 28))
@@ -106,7 +106,10 @@ def _scaling_closed_form(cfg, Xs, X2s=None):
         return False
     d, M = Xs.shape[-1], cfg["num_levels"]
     n = Xs.shape[0] + (0 if X2s is None else X2s.shape[0])
-    return 8 * n * sum(d ** m for m in range(1, M + 1)) <= SCALING_FEATURE_BYTES
+    ln = max(Xs.shape[1], 1 if X2s is None else X2s.shape[1])
+    ch = sum(d ** m for m in range(1, M + 1))
+    # the features themselves and one sequence's step exponentials in _signature64 (three live copies)
+    return 8 * n * ch <= SCALING_FEATURE_BYTES and 24 * max(ln - 1, 1) * ch <= SCALING_FEATURE_BYTES
 
 
 def _signature64(X, M):
@@ -157,7 +160,7 @@ def _scaling_contraction(Xs, X2s, M, gK, gd1=None, gd2=None):
             v = v + (gd1[m].double()[:, None] * P * P).sum(0)
         if gd2 is not None:
             v = v + (gd2[m].double()[:, None] * Q * Q).sum(0)
-        e += 2.0 * (v @ _word_counts(d, m, Xs.device))
+        e += 2.0 * _channel_counts(v, d, m)
         off += w
     return e
 
