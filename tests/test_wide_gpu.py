@@ -529,3 +529,22 @@ def test_wide_split_operand_scales(case):
     sym = ops.sig_gram(t(X), None, M, base=base).cpu().numpy()
     err = norm_rel_err(sym[1:], ref.K_seq(X)[1:], axis_levels=True)
     assert (err < TOL).all(), err
+
+
+@pytest.mark.parametrize("M", [1, 2, 7, 8])
+@pytest.mark.parametrize("L", [60, 150])
+def test_wide_matrix_core_level_counts(M, L):
+    """The matrix-core wide Gram (sig_fo_mf.h) at the level counts the other wide tests do not reach (level 1 alone
+    is the closed form; 7 and 8 levels at W = 4 / 10 columns per lane), raw levels vs the fp64 oracle."""
+    from gpsig_amd import ops
+    rng = np.random.default_rng(M * 100 + L)
+    D = 40
+    X = walks(rng, 4, L, D)
+    Y = walks(rng, 3, L - 3, D)
+    ref = kr.SignatureKernelRef(L * D, D, M, normalization=False)
+    got = ops.sig_gram(t(X), t(Y), M).cpu().numpy()
+    err = norm_rel_err(got[1:], ref.K_seq(X, Y)[1:], axis_levels=True)
+    assert (err < TOL).all(), err
+    sym = ops.sig_gram(t(X), None, M).cpu().numpy()
+    err = norm_rel_err(sym[1:], ref.K_seq(X)[1:], axis_levels=True)
+    assert (err < TOL).all(), err
