@@ -1,6 +1,8 @@
 #!/bin/bash
 # Round 6 forward A/B (tools/kbench.hip): scalar record loads (GPSIG_SREC) and the scans issued before the
 # row's cells (GPSIG_SCAN_FIRST 1: prefixes kept live, 2: recomputed) at C2 (W10/LP10), H (W8/LP16) and C5.
+# (Both switches were removed from the sources after this A/B -- gpurun_out/r6h, DESIGN.md 2.1: -0.4 % and 2x
+#  slower -- so rebuilding these variants now gives four copies of the kept kernel.)
 set -e
 cd "$(dirname "$0")/.."
 mkdir -p tools/bin
