@@ -220,8 +220,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(GPSIG_BWD_W
 #ifndef GPSIG_BWD_RC
 #define GPSIG_BWD_RC 4
 #endif
-  // rows per chunk of the reverse sweep (LDS: 4 waves x RC x 64 lanes x 2W floats per workgroup)
-  constexpr int RC = W >= 4 ? GPSIG_BWD_RC : 8;
+  // rows per chunk of the reverse sweep (LDS: 4 waves x RC x 64 lanes x 2W floats per workgroup); the 20-lane
+  // geometry (C2's 65-100 points) regenerates 6 rows per exact row: 21.73 -> 21.45 ms on tools/kbench_vjp.hip
+  // (profiles/r6_vjp_rc_ab.txt), the other geometries keep 4 (round 3: 6 within noise there)
+  constexpr int RC = W >= 4 ? (LP == 20 ? 6 : GPSIG_BWD_RC) : 8;
   __shared__ __attribute__((aligned(16))) float cbuf[RBF && DIFF ? 4 : 1][RBF && DIFF ? RC : 1][64][2 * W];
   __shared__ float tbuf[DP <= 8 ? 4 : 1][DP <= 8 ? 4 : 1][DP <= 8 ? DP : 1][64];  // x-gradient row batches
   constexpr int ML = M > 1 ? M - 1 : 1;
