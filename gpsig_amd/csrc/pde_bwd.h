@@ -67,9 +67,12 @@ GPSIG_DEV float tile_inc_b(const float *__restrict__ base, long long ld, int sub
   return sub ? v * __builtin_ldexpf(1.0f, -2 * sub) : v;
 }
 
-// coarse steps per stored front: the chunk's K corners (H x REP x W floats per lane) live in registers
+// coarse steps per stored front: the chunk's K corners (H x REP x W <= GPSIG_PDE_HF floats per lane) live in registers
+#ifndef GPSIG_PDE_HF
+#define GPSIG_PDE_HF 32
+#endif
 template <int W, int REP>
-constexpr int pde_chunk() { return REP * W >= 32 ? 1 : 32 / (REP * W); }
+constexpr int pde_chunk() { return REP * W >= GPSIG_PDE_HF ? 1 : GPSIG_PDE_HF / (REP * W); }
 
 // Columns per lane of the adjoint kernel: the smallest power of two >= REP with ceil(J / W) <= 64 lanes,
 // else the widest the registers take (REP * W <= 64, W <= 16) and the grid is swept in column blocks of
@@ -99,7 +102,7 @@ __host__ __device__ inline PdeLayout pde_layout(int l1, int l2, int dyadic) {
   const int J = (int)JL, W = pde_bwd_cols(J, rep);
   if (W == 0) return L;
   L.W = W;
-  L.H = rep * W >= 32 ? 1 : 32 / (rep * W);
+  L.H = rep * W >= GPSIG_PDE_HF ? 1 : GPSIG_PDE_HF / (rep * W);
   const long long CB = 64LL * W;
   L.nblk = (int)((J + CB - 1) / CB);
   const long long U = L.nblk == 1 ? (J + W - 1) / W : 64;
