@@ -255,7 +255,7 @@ struct RbfSeedPk {
   static constexpr int W2 = W / 2;
   static constexpr int FS = feat_stride(DP);
 #ifndef GPSIG_PK_ANCHOR
-#define GPSIG_PK_ANCHOR 64
+#define GPSIG_PK_ANCHOR 128
 #endif
   static constexpr int ANCHOR = GPSIG_PK_ANCHOR;
   static constexpr float NHL2E = -0.72134752044448170f;  // exp(-d2/2) = exp2(d2 * NHL2E)
