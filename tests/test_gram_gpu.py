@@ -295,3 +295,19 @@ def test_seed_regimes(scale, jumps, D):
     got = k.K(t(X.reshape(N, -1)), return_levels=True).cpu().numpy()
     exp = kr.SignatureKernelRef(L * D, D, M).K(X.reshape(N, -1), return_levels=True)
     assert (norm_rel_err(got, exp, axis_levels=True) < TOL).all()
+
+
+@pytest.mark.parametrize("scale,D,M", [(0.01, 5, 5), (0.06, 5, 5), (0.03, 8, 6)])
+def test_anchor_spans_long_sequences(scale, D, M):
+    """Sequences of 480 points: the packed recurrences (k by (1 + expm1(p)), Eq by the expm1 chain) run for
+    GPSIG_PK_ANCHOR = 128 rows between exact re-evaluations, four spans per pair here; the accumulated
+    rounding must stay inside the parity tolerance against the oracle (small and medium increments, and
+    D = 8, whose column pairs >= 1 re-read their points on anchor rows)."""
+    import gpsig_amd
+    rng = np.random.default_rng(23)
+    N, L = 5, 480
+    X = np.cumsum(rng.standard_normal((N, L, D)) * scale, 1)
+    k = gpsig_amd.SignatureRBF(L * D, D, M)
+    got = k.K(t(X.reshape(N, -1)), return_levels=True).cpu().numpy()
+    exp = kr.SignatureKernelRef(L * D, D, M).K(X.reshape(N, -1), return_levels=True)
+    assert (norm_rel_err(got, exp, axis_levels=True) < TOL).all()
